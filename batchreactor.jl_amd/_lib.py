@@ -1,0 +1,76 @@
+"""ctypes binding of libbrhip.so (include/brhip.h). Fails loudly when the library is absent:
+there is no CPU fallback in the product path."""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, "libbrhip.so")
+
+dp = C.POINTER(C.c_double)
+ip = C.POINTER(C.c_int)
+
+
+class MechDesc(C.Structure):
+    _fields_ = [
+        ("ng", C.c_int), ("ns", C.c_int), ("nrg", C.c_int), ("nrs", C.c_int),
+        ("conv", C.c_int), ("p_std", C.c_double),
+        ("molwt", dp), ("nasa", dp),
+        ("g_nf", ip), ("g_nr", ip), ("g_f", ip), ("g_r", ip), ("g_rev", ip), ("g_tb", ip),
+        ("g_arr", dp), ("g_low", dp), ("g_troe_n", ip), ("g_troe", dp), ("g_eff", dp),
+        ("site_density", C.c_double), ("sigma", dp),
+        ("s_nf", ip), ("s_np", ip), ("s_f", ip), ("s_p", ip), ("s_stick", ip), ("s_arr", dp),
+        ("s_ncov", ip), ("s_cov_sp", ip), ("s_cov_eps", dp),
+    ]
+
+
+class Opts(C.Structure):
+    _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("max_steps", C.c_int), ("device", C.c_int),
+                ("hmax", C.c_double)]
+
+
+EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info",
+           "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_dev", "br_last_kernel_ms"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIBPATH):
+        raise RuntimeError(f"libbrhip.so not built ({LIBPATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIBPATH)
+    vp = C.c_void_p
+    L.br_version.restype = C.c_int
+    L.br_last_error.restype = C.c_char_p
+    L.br_device_count.restype = C.c_int
+    L.br_mech_create.argtypes = [C.POINTER(MechDesc), C.c_int, C.POINTER(vp)]
+    L.br_mech_destroy.argtypes = [vp]
+    L.br_mech_info.argtypes = [vp, ip, ip, ip, ip]
+    L.br_rates.argtypes = [vp, C.c_int, dp, dp, dp, dp, dp, dp]
+    L.br_rhs.argtypes = [vp, C.c_int, dp, dp, dp, dp]
+    L.br_jacobian.argtypes = [vp, C.c_int, dp, dp, dp, dp]
+    L.br_integrate.argtypes = [vp, C.c_int, dp, dp, dp, dp, C.POINTER(Opts), dp]
+    L.br_integrate_dev.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.POINTER(Opts), vp, vp]
+    L.br_last_kernel_ms.argtypes = [vp, dp]
+    for f in ("br_mech_create", "br_mech_destroy", "br_mech_info", "br_rates", "br_rhs", "br_jacobian",
+              "br_integrate", "br_integrate_dev", "br_last_kernel_ms"):
+        getattr(L, f).restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(f"libbrhip error {rc}: {lib().br_last_error().decode()}")
+
+
+def dptr(a):
+    return a.ctypes.data_as(dp) if a is not None else None
+
+
+def iptr(a):
+    return a.ctypes.data_as(ip)

@@ -1,0 +1,117 @@
+"""Engine: a compiled mechanism resident on one GPU (br_mech handle) and the batched hot-path
+operators on it. This is the host mirror of the reference's operator interface:
+
+  rates(...)      <- GasphaseReactions / SurfaceReactions.calculate_molar_production_rates!
+                     (src/BatchReactor.jl:344,:355), batched
+  rhs(...)        <- residual!(du,u,p,t) (src/BatchReactor.jl:312-376), batched
+  jacobian(...)   <- the dense Jacobian CVODE forms inside CVODE_BDF() (:138-141,:210)
+  integrate(...)  <- solve(ODEProblem(residual!,u0,(0,tf),params), CVODE_BDF();
+                     reltol=1e-6, abstol=1e-10, save_everystep=false) (:138-141,:204-210)
+
+Arrays are reactor-major: u[N, n], n = ng + ns, u = [rho*Y_k ; theta_k].
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .mechanism import Mechanism
+
+STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status")
+
+
+class Engine:
+    def __init__(self, mech: Mechanism, device: int = 0):
+        L = _lib.lib()
+        self.mech = mech
+        self.device = device
+        t = mech.tables
+        self._keep = []
+
+        def d(a):
+            a = np.ascontiguousarray(a, dtype=np.float64)
+            self._keep.append(a)
+            return _lib.dptr(a)
+
+        def i(a):
+            a = np.ascontiguousarray(a, dtype=np.int32)
+            self._keep.append(a)
+            return _lib.iptr(a)
+
+        desc = _lib.MechDesc(
+            mech.ng, mech.ns, mech.nrg, mech.nrs, mech.conv, mech.p_std,
+            d(mech.molwt), d(mech.nasa),
+            i(t["g_nf"]), i(t["g_nr"]), i(t["g_f"]), i(t["g_r"]), i(t["g_rev"]), i(t["g_tb"]),
+            d(t["g_arr"]), d(t["g_low"]), i(t["g_troe_n"]), d(t["g_troe"]), d(t["g_eff"]),
+            mech.site_density, d(mech.sigma),
+            i(t["s_nf"]), i(t["s_np"]), i(t["s_f"]), i(t["s_p"]), i(t["s_stick"]), d(t["s_arr"]),
+            i(t["s_ncov"]), i(t["s_cov_sp"]), d(t["s_cov_eps"]))
+        h = C.c_void_p()
+        _lib.check(L.br_mech_create(C.byref(desc), device, C.byref(h)))
+        self.h = h
+        self.n, self.ng, self.ns = mech.n, mech.ng, mech.ns
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().br_mech_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _arr(a, N, dtype=np.float64):
+        return np.ascontiguousarray(np.broadcast_to(np.asarray(a, dtype), (N,)))
+
+    def rates(self, T, p, x, theta=None):
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float64)
+        N = x.shape[0]
+        T, p = self._arr(T, N), self._arr(p, N)
+        th = None if (theta is None or self.ns == 0) else np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+        w = np.zeros((N, self.ng))
+        s = np.zeros((N, self.n))
+        _lib.check(_lib.lib().br_rates(self.h, N, _lib.dptr(T), _lib.dptr(p), _lib.dptr(x), _lib.dptr(th),
+                                       _lib.dptr(w), _lib.dptr(s)))
+        return w, s
+
+    def rhs(self, T, Asv, u):
+        u = np.ascontiguousarray(np.atleast_2d(u), dtype=np.float64)
+        N = u.shape[0]
+        T, A = self._arr(T, N), self._arr(Asv, N)
+        du = np.zeros_like(u)
+        _lib.check(_lib.lib().br_rhs(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(du)))
+        return du
+
+    def jacobian(self, T, Asv, u):
+        u = np.ascontiguousarray(np.atleast_2d(u), dtype=np.float64)
+        N = u.shape[0]
+        T, A = self._arr(T, N), self._arr(Asv, N)
+        J = np.zeros((N, self.n, self.n))
+        _lib.check(_lib.lib().br_jacobian(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(J)))
+        return J
+
+    def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000):
+        u = np.array(np.atleast_2d(u0), dtype=np.float64, order="C")
+        N = u.shape[0]
+        T, A, tf = self._arr(T, N), self._arr(Asv, N), self._arr(tf, N)
+        st = np.zeros((N, 8))
+        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0)
+        _lib.check(_lib.lib().br_integrate(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(tf),
+                                           C.byref(o), _lib.dptr(st)))
+        return u, {k: st[:, i] for i, k in enumerate(STAT_FIELDS)}
+
+    def integrate_device(self, T_ptr, Asv_ptr, u_ptr, tf_ptr, stats_ptr, N, stream_ptr=None, rtol=1e-6,
+                         atol=1e-10, max_steps=100000):
+        """Device-resident variant: raw device pointers (e.g. torch tensor data_ptr())."""
+        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0)
+        _lib.check(_lib.lib().br_integrate_dev(self.h, N, C.c_void_p(T_ptr), C.c_void_p(Asv_ptr),
+                                               C.c_void_p(u_ptr), C.c_void_p(tf_ptr), C.byref(o),
+                                               C.c_void_p(stats_ptr), C.c_void_p(stream_ptr or 0)))
+
+    def last_kernel_ms(self):
+        ms = np.zeros(1)
+        _lib.check(_lib.lib().br_last_kernel_ms(self.h, _lib.dptr(ms)))
+        return float(ms[0])

@@ -1,0 +1,122 @@
+/*
+ * brhip.h -- C-ABI of libbrhip.so, the MI355X (gfx950) batched stiff-kinetics engine that
+ * sits behind BatchReactor.jl's hot path. Plain C types only; fp64 everywhere; int status
+ * return (0 = OK, negative = error class, message via br_last_error()).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference root):
+ *   br_mech_create   <- compile_gaschemistry / SurfaceReactions.compile_mech /
+ *                       IdealGas.create_thermo results (src/BatchReactor.jl:254,265,287):
+ *                       the host flattens the compiled mechanism into br_mech_desc.
+ *   br_rates         <- GasphaseReactions.calculate_molar_production_rates!(g_state,gmd,thermo)
+ *                       (call site src/BatchReactor.jl:355) and
+ *                       SurfaceReactions.calculate_molar_production_rates!(s_state,thermo,smd)
+ *                       (call site :344), batched over N states.
+ *   br_rhs           <- residual!(du,u,p,t) (src/BatchReactor.jl:312-376), batched.
+ *   br_jacobian      <- the dense Jacobian CVODE builds by finite differences inside
+ *                       solve(..., CVODE_BDF()) (:138-141, :208-210); here analytic.
+ *   br_integrate     <- solve(ODEProblem(residual!,u0,(0,tf),params), CVODE_BDF();
+ *                       reltol=1e-6, abstol=1e-10, save_everystep=false)
+ *                       (src/BatchReactor.jl:138-141 and :204-210), for N reactors at once.
+ *   br_integrate_dev <- same, device-resident buffers on a caller stream (ensemble driver).
+ *
+ * Layout: per-reactor rows, reactor-major: u[N][n] with n = ng + ns and
+ * u_k = rho*Y_k (kg/m3) for k < ng, theta_k for ng <= k < n (src/BatchReactor.jl:224-231).
+ * A handle may be used by one host thread at a time; there is no global state.
+ */
+#ifndef BRHIP_H
+#define BRHIP_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BR_OK             0
+#define BR_ERR_MAXSTEPS  -1   /* CVODE CV_TOO_MUCH_WORK  */
+#define BR_ERR_ERRTEST   -3   /* CVODE CV_ERR_FAILURE     */
+#define BR_ERR_CONV      -4   /* CVODE CV_CONV_FAILURE    */
+#define BR_ERR_INPUT    -10
+#define BR_ERR_HIP      -20
+#define BR_ERR_UNSUPPORTED -30
+
+/* convention switches (bitmask); see DESIGN.md "Parity status" */
+#define BR_CONV_KC_UNIT_SLIP  1   /* Kc *= (1e6)^dnu for non-falloff reversible reactions */
+#define BR_CONV_FALLOFF_XM    2   /* falloff net rate *= [M]                              */
+#define BR_CONV_DOC_COVG      4   /* no Asv on dtheta/dt (docs sample, predates :345)     */
+
+typedef struct br_mech br_mech;
+
+typedef struct br_mech_desc {
+    int ng, ns, nrg, nrs;
+    int conv;                 /* BR_CONV_* bitmask                                 */
+    double p_std;             /* standard pressure for Kc [Pa]                     */
+    const double* molwt;      /* [ng] kg/mol                                       */
+    const double* nasa;       /* [ng][15]: Tmid, a_hi[7], a_lo[7] (NASA-7)         */
+    /* gas reactions (CHEMKIN-II) */
+    const int* g_nf;          /* [nrg] expanded reactant entries (<=4)             */
+    const int* g_nr;          /* [nrg] expanded product entries  (<=4)             */
+    const int* g_f;           /* [nrg][4] species index per entry, -1 pad          */
+    const int* g_r;           /* [nrg][4]                                          */
+    const int* g_rev;         /* [nrg] 1 reversible                                */
+    const int* g_tb;          /* [nrg] 0 none, 1 third body (+M), 2 falloff (+M)   */
+    const double* g_arr;      /* [nrg][3] A (SI), beta, Ea/R [K] (k_inf if falloff) */
+    const double* g_low;      /* [nrg][3] k0: A (SI), beta, E/R                    */
+    const int* g_troe_n;      /* [nrg] 0 Lindemann, else number of Troe params 3|4 */
+    const double* g_troe;     /* [nrg][4] a, T***, T*, T**                         */
+    const double* g_eff;      /* [nrg][ng] third-body efficiencies (tb rows)       */
+    /* surface reactions */
+    double site_density;      /* mol/cm2                                           */
+    const double* sigma;      /* [ns] site coordination                           */
+    const int* s_nf;          /* [nrs] <=6                                         */
+    const int* s_np;          /* [nrs] <=6                                         */
+    const int* s_f;           /* [nrs][6] combined index: gas 0..ng-1, surface ng.. */
+    const int* s_p;           /* [nrs][6]                                          */
+    const int* s_stick;       /* [nrs] 1 sticking coefficient reaction             */
+    const double* s_arr;      /* [nrs][3] A (SI) or s0, beta, Ea [J/mol]           */
+    const int* s_ncov;        /* [nrs] coverage-dependent terms (<=4)              */
+    const int* s_cov_sp;      /* [nrs][4] combined species index                  */
+    const double* s_cov_eps;  /* [nrs][4] J/mol                                    */
+} br_mech_desc;
+
+typedef struct br_opts {
+    double rtol, atol;        /* default 1e-6 / 1e-10 (src/BatchReactor.jl:141,:210) */
+    int max_steps;            /* default 100000 (Sundials.jl maxiters)             */
+    int device;               /* HIP device ordinal for br_mech_create             */
+    double hmax;              /* 0 = unbounded                                     */
+} br_opts;
+
+typedef struct br_stats {     /* per reactor, counters as CVODE's                  */
+    double nsteps, nfe, nje, nsetups, nni, ncfn, netf, status;
+} br_stats;
+
+int         br_version(void);
+const char* br_last_error(void);
+int         br_device_count(void);
+
+int br_mech_create(const br_mech_desc* desc, int device, br_mech** out);
+int br_mech_destroy(br_mech* m);
+int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs);
+
+/* host-buffer entry points (copy in/out); arrays are reactor-major */
+int br_rates(br_mech* m, int N, const double* T, const double* p, const double* x /*[N][ng]*/,
+             const double* theta /*[N][ns] or NULL*/, double* wdot /*[N][ng]*/,
+             double* sdot /*[N][ng+ns] or NULL*/);
+int br_rhs(br_mech* m, int N, const double* T, const double* Asv, const double* u /*[N][n]*/,
+           double* du /*[N][n]*/);
+int br_jacobian(br_mech* m, int N, const double* T, const double* Asv, const double* u,
+                double* J /*[N][n][n] row-major d(du_i)/d(u_j)*/);
+int br_integrate(br_mech* m, int N, const double* T, const double* Asv, double* u /*in/out*/,
+                 const double* tf, const br_opts* opts, br_stats* stats /*[N] or NULL*/);
+
+/* device-buffer entry point: all pointers are device memory on m's device; `stream` is a
+ * hipStream_t (NULL = default stream). Asynchronous: returns after the launch. */
+int br_integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv, double* du,
+                     const double* dtf, const br_opts* opts, br_stats* dstats, void* stream);
+
+/* timing helper for roofline accounting: duration (ms) of the last integrate kernel,
+ * measured with HIP events on the stream it was launched on (after the stream syncs). */
+int br_last_kernel_ms(br_mech* m, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,183 @@
+"""Parity of the HIP path (libbrhip.so, called through the C-ABI) against the CPU oracle.
+
+Tolerances (north_star: production rates within 1e-12 relative; trajectories within 1e-4):
+  * rates / RHS: |gpu - oracle| <= 1e-12 * scale_k, scale_k = sum_r |nu_kr q_r| (the magnitude
+    of the terms summed into species k, so near-equilibrium cancellation is judged against
+    the size of the contributions, not against their tiny difference) + 1e-300;
+  * Jacobian: row-wise 1e-11 * max_j |J_kj|;
+  * integrated states: 1e-4 relative on components above 1e-8 of the largest one.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import LIB
+
+pytestmark = pytest.mark.gpu
+TH = os.path.join(LIB, "therm.dat")
+SURF_GAS = ["CH4", "H2O", "H2", "CO", "CO2", "O2", "N2"]
+
+CASES = {
+    "h2o2": dict(gas="h2o2.dat", surf=None),
+    "gri": dict(gas="grimech.dat", surf=None),
+    "surf": dict(gas=None, surf="ch4ni.xml"),
+}
+
+
+def _mechs(pkg, orc, case, conv=0):
+    c = CASES[case]
+    gm = c["gas"]
+    pm = pkg.Mechanism.from_files(LIB, gas_mech=gm, surface_mech=c["surf"], gasphase=None if gm else SURF_GAS, conv=conv)
+    om = orc.Mech(os.path.join(LIB, gm) if gm else None, TH, os.path.join(LIB, c["surf"]) if c["surf"] else None,
+                  gas_species=None if gm else SURF_GAS, conv=conv)
+    return pm, om
+
+
+def _states(pm, N, seed):
+    rng = np.random.default_rng(seed)
+    T = rng.uniform(900.0, 1400.0, N)
+    p = np.exp(rng.uniform(np.log(0.5e5), np.log(1e6), N))
+    x = rng.random((N, pm.ng)) ** 4 + 1e-12
+    x /= x.sum(1, keepdims=True)
+    th = rng.random((N, pm.ns)) ** 3 + 1e-14
+    if pm.ns:
+        th /= th.sum(1, keepdims=True)
+    return T, p, x, th
+
+
+def _scale(pm, qg, qs):
+    """sum_r |nu_kr q_r| per species."""
+    t = pm.tables
+    sc = np.zeros(pm.n)
+    for r in range(pm.nrg):
+        for e in range(t["g_nf"][r]):
+            sc[t["g_f"][r, e]] += abs(qg[r])
+        for e in range(t["g_nr"][r]):
+            sc[t["g_r"][r, e]] += abs(qg[r])
+    for r in range(pm.nrs):
+        for e in range(t["s_nf"][r]):
+            sc[t["s_f"][r, e]] += abs(qs[r])
+        for e in range(t["s_np"][r]):
+            sc[t["s_p"][r, e]] += abs(qs[r])
+    return sc
+
+
+@pytest.mark.parametrize("case", ["h2o2", "gri", "surf"])
+def test_rates_parity(pkg, orc, gpu, case):
+    pm, om = _mechs(pkg, orc, case)
+    eng = pkg.Engine(pm)
+    N = 64
+    T, p, x, th = _states(pm, N, 11)
+    w, s = eng.rates(T, p, x, th if pm.ns else None)
+    for i in range(N):
+        wo, so = om.rates(T[i], p[i], x[i], th[i] if pm.ns else None)
+        qg, qs = om.rop(T[i], p[i], x[i], th[i] if pm.ns else None)
+        sc = _scale(pm, qg, qs)
+        assert np.all(np.abs(w[i] - wo) <= 1e-12 * sc[:pm.ng] + 1e-300), (case, i)
+        if pm.ns:
+            assert np.all(np.abs(s[i] - so) <= 1e-12 * sc + 1e-300), (case, i)
+
+
+@pytest.mark.parametrize("case", ["h2o2", "gri", "surf"])
+def test_rhs_and_jacobian_parity(pkg, orc, gpu, case):
+    pm, om = _mechs(pkg, orc, case)
+    eng = pkg.Engine(pm)
+    N = 16
+    T, p, x, th = _states(pm, N, 12)
+    Asv = np.exp(np.random.default_rng(3).uniform(0, np.log(100), N))
+    U = np.stack([pm.initial_state(T[i], p[i], x[i], th[i] if pm.ns else None) for i in range(N)])
+    du = eng.rhs(T, Asv, U)
+    J = eng.jacobian(T, Asv, U)
+    for i in range(N):
+        do, pp, xx = om.rhs(T[i], Asv[i], U[i])
+        Jo = om.jac(T[i], Asv[i], U[i])
+        scale = np.abs(Jo).max(1) * np.abs(U[i]).max() + np.abs(do) + 1e-300
+        assert np.all(np.abs(du[i] - do) <= 1e-11 * scale), (case, i)
+        js = np.abs(Jo).max(1, keepdims=True) + 1e-300
+        assert np.max(np.abs(J[i] - Jo) / js) < 1e-11, (case, i)
+
+
+def _ignition_inputs(pm, case, N, seed):
+    rng = np.random.default_rng(seed)
+    if case == "surf":
+        T = rng.uniform(973.0, 1173.0, N)
+        p = np.full(N, 1e5)
+        sc = rng.uniform(1, 3, N)
+        X = np.zeros((N, pm.ng))
+        X[:, pm.gas_species.index("CH4")] = 0.5 / (1 + sc)
+        X[:, pm.gas_species.index("H2O")] = 0.5 * sc / (1 + sc)
+        X[:, pm.gas_species.index("N2")] = 0.5
+        Asv = np.exp(rng.uniform(0, np.log(100), N))
+    elif case == "h2o2":
+        T = rng.uniform(1000.0, 1400.0, N)
+        p = np.exp(rng.uniform(np.log(0.5e5), np.log(1e6), N))
+        phi = np.exp(rng.uniform(np.log(0.5), np.log(2), N))
+        X = np.zeros((N, pm.ng))
+        X[:, pm.gas_species.index("H2")] = 0.5 * 2 * phi / (2 * phi + 1)
+        X[:, pm.gas_species.index("O2")] = 0.5 / (2 * phi + 1)
+        X[:, pm.gas_species.index("N2")] = 0.5
+        Asv = np.ones(N)
+    else:
+        T = rng.uniform(1100.0, 1300.0, N)
+        p = np.exp(rng.uniform(np.log(1e5), np.log(1e6), N))
+        phi = rng.uniform(0.5, 1.5, N)
+        X = np.zeros((N, pm.ng))
+        X[:, pm.gas_species.index("CH4")] = 0.75 * phi / (phi + 2)
+        X[:, pm.gas_species.index("O2")] = 1.5 / (phi + 2)
+        X[:, pm.gas_species.index("N2")] = 0.25
+        Asv = np.ones(N)
+    U = np.stack([pm.initial_state(T[i], p[i], X[i]) for i in range(N)])
+    return T, Asv, U
+
+
+@pytest.mark.parametrize("case,N,tf", [("h2o2", 32, 10.0), ("gri", 8, 10.0), ("surf", 16, 10.0)])
+def test_integrate_parity(pkg, orc, gpu, case, N, tf):
+    pm, om = _mechs(pkg, orc, case)
+    eng = pkg.Engine(pm)
+    T, Asv, U0 = _ignition_inputs(pm, case, N, 5)
+    U, st = eng.integrate(T, Asv, U0, tf)
+    assert np.all(st["status"] == 0)
+    Uo, sto, bad = om.integrate_batch(T, Asv, U0, tf, analytic_jac=True, nthreads=4)
+    assert bad == 0
+    for i in range(N):
+        big = np.abs(Uo[i]) > 1e-8 * np.abs(Uo[i]).max()
+        rel = np.max(np.abs(U[i][big] / Uo[i][big] - 1))
+        assert rel < 1e-4, (case, i, rel)
+        # same algorithm -> same step count up to rounding-induced path differences
+        assert abs(st["nsteps"][i] - sto[i]["nsteps"]) <= 0.1 * sto[i]["nsteps"] + 5
+
+
+def test_integrate_edge_cases(pkg, orc, gpu):
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", 4, 9)
+    U, st = eng.integrate(T[:0], Asv[:0], U0[:0], 1.0)                  # empty ensemble
+    assert U.shape == (0, pm.n)
+    tf = np.array([1e-6, 1e-3, 1.0, 10.0])                              # ragged end times
+    U, st = eng.integrate(T, Asv, U0, tf)
+    for i in range(4):
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf[i], analytic_jac=True)
+        big = np.abs(uo) > 1e-8 * np.abs(uo).max()
+        assert np.max(np.abs(U[i][big] / uo[big] - 1)) < 1e-4
+    U1, st1 = eng.integrate(T[:1], Asv[:1], U0[:1], 10.0, max_steps=5)  # step limit -> CV_TOO_MUCH_WORK
+    assert st1["status"][0] == -1
+
+
+def test_mass_conservation_full_size(pkg, gpu):
+    """Size-independent property at a large ensemble: total gas mass is invariant for gas-only
+    chemistry (sum_k du_k = 0), so sum(u) at tf equals sum(u0) to the integration tolerance."""
+    pm = pkg.Mechanism.from_files(LIB, gas_mech="h2o2.dat")
+    eng = pkg.Engine(pm)
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", 4096, 21)
+    U, st = eng.integrate(T, Asv, U0, 1.0)
+    assert np.all(st["status"] == 0)
+    np.testing.assert_allclose(U.sum(1), U0.sum(1), rtol=1e-6)
+
+
+def test_programmatic_api(pkg, gpu):
+    """batch_reactor(inlet_comp, T, p, time; chem, thermo_obj, md) (test/runtests.jl:51-67)."""
+    m = pkg.Mechanism.from_files(LIB, gas_mech="h2o2.dat")
+    t, xd = pkg.batch_reactor_programmatic({"O2": 0.25, "N2": 0.5, "H2": 0.25}, 1073.15, 1e5, 10.0,
+                                           chem=pkg.Chemistry(gaschem=True), mech=m)
+    assert t[-1] == 10.0 and abs(sum(xd.values()) - 1) < 1e-12

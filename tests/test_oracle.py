@@ -1,0 +1,154 @@
+"""Pins the CPU oracle against the reference's own data (CPU only, no GPU).
+
+Fixtures (tests/golden/, built by tests/golden/make_golden.py from the reference):
+  * gas_and_surf_golden.csv / gas_and_surf_covg_golden.csv -- test/batch_gas_and_surf/*.csv,
+    written by the reference (Julia + CVODE_BDF, rtol 1e-6, atol 1e-10)
+  * doc_surf_rows.csv -- docs/src/index.md:160-185 (surface-only sample output)
+"""
+import csv
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, LIB
+
+TH = os.path.join(LIB, "therm.dat")
+SURF_GAS = ["CH4", "H2O", "H2", "CO", "CO2", "O2", "N2"]
+
+
+def _golden(name):
+    rows = list(csv.reader(open(os.path.join(GOLDEN, name))))
+    return rows[0][1:], np.array([[float(v) for v in r[1:]] for r in rows[1:]]), [int(r[0]) for r in rows[1:]]
+
+
+@pytest.fixture(scope="module")
+def gs_mech(orc):
+    return orc.Mech(os.path.join(LIB, "grimech.dat"), TH, os.path.join(LIB, "ch4ni.xml"))
+
+
+def gs_u0(m):
+    x = np.zeros(m.ng)
+    x[m.names.index("CH4")], x[m.names.index("O2")], x[m.names.index("N2")] = 0.25, 0.5, 0.25
+    return m.initial_state(1173.0, 1e5, x)
+
+
+def test_mechanism_sizes(orc, gs_mech):
+    # SURVEY.md section 0 item 8 / Appendix B
+    assert (gs_mech.ng, gs_mech.ns, gs_mech.nrg, gs_mech.nrs) == (53, 13, 325, 42)
+    h = orc.Mech(os.path.join(LIB, "h2o2.dat"), TH)
+    assert (h.ng, h.nrg) == (9, 18)
+    assert gs_mech.site_density == pytest.approx(2.66e-9)
+    np.testing.assert_array_equal(gs_mech.theta0[[0, 4]], [0.6, 0.4])
+
+
+def test_initial_density_bit_exact(gs_mech):
+    """rho0 of the golden row 0 (IdealGas.density, src/BatchReactor.jl:226-227)."""
+    hdr, g, _ = _golden("gas_and_surf_golden.csv")
+    u0 = gs_u0(gs_mech)
+    assert u0[:gs_mech.ng].sum() == g[0, 3] == 0.27697974868307573
+
+
+def test_pressure_diagnosis_matches_golden(gs_mech):
+    """p = rho R T / Mbar (src/BatchReactor.jl:338,:353) on every golden row (x, p from the same RHS call)."""
+    hdr, g, _ = _golden("gas_and_surf_golden.csv")
+    R = 8.31446261815324
+    x = g[:, 4:]
+    Mb = x @ gs_mech.M
+    p = g[:, 3] * R * 1173.0 / Mb
+    assert np.max(np.abs(p / g[:, 2] - 1)) < 1e-10
+
+
+def test_first_cvode_step_bit_exact(gs_mech):
+    """cvHin on the reference RHS at t=0 reproduces the golden first step time exactly."""
+    hdr, g, _ = _golden("gas_and_surf_golden.csv")
+    u, st, rows = gs_mech.integrate(1173.0, 1.0, gs_u0(gs_mech), 10.0, record=True, max_steps=3)
+    assert rows[1][0] == g[1, 0] == 4.3211443386069156e-16
+
+
+def test_golden_early_surface_trajectory(gs_mech):
+    """The first 11 accepted steps of one run to tf = 10 s against golden rows 1-11 (consecutive
+    steps). Step times agree to 1e-4 and coverages / surface-driven gas species to 1e-4 relative
+    (species above 1e-12). Rows hold the state of the last RHS call (save_data, :383-402)."""
+    hdr, g, idx = _golden("gas_and_surf_golden.csv")
+    _, s, _ = _golden("gas_and_surf_covg_golden.csv")
+    u, st, rows = gs_mech.integrate(1173.0, 1.0, gs_u0(gs_mech), 10.0, record=True, max_steps=12)
+    assert idx[:12] == list(range(12))
+    for i in range(1, 12):
+        t, uu, p, x, th = rows[i]
+        assert abs(t / g[i, 0] - 1) < 1e-4, i
+        gth = s[i, 2:]
+        big = gth > 1e-12
+        assert np.max(np.abs(th[big] / gth[big] - 1)) < 1e-4, (i, t)
+        for name in ("H2O", "CH4", "O2", "N2"):
+            k = gs_mech.names.index(name)
+            assert abs(x[k] / g[i, 4 + k] - 1) < 1e-4
+        assert abs(p / g[i, 2] - 1) < 1e-9
+
+
+def test_doc_surface_rows(orc):
+    """docs/src/index.md:160-185 (batch_surf inputs, Asv = 10). The sample predates
+    src/BatchReactor.jl:345 (no Asv on dtheta/dt) -> CONV_DOC_COVG. Late-time rows to 2e-3."""
+    m = orc.Mech(None, TH, os.path.join(LIB, "ch4ni.xml"), gas_species=SURF_GAS, conv=orc.CONV_DOC_COVG)
+    x = np.zeros(m.ng)
+    x[0], x[1], x[6] = 0.25, 0.25, 0.5
+    u0 = m.initial_state(1073.15, 1e5, x)
+    rows = list(csv.reader(open(os.path.join(GOLDEN, "doc_surf_rows.csv"))))
+    gas = {float(r[2]): np.array([float(v) for v in r[6:]]) for r in rows if r[1] == "gas"}
+    surf = {float(r[2]): np.array([float(v) for v in r[4:]]) for r in rows if r[1] == "surf"}
+    checked = 0
+    for t in (7.3222e-12, 9.8894, 9.984, 10.0):
+        u, st, _ = m.integrate(1073.15, 10.0, u0, t)
+        xs = u[:m.ng] / m.M
+        xs /= xs.sum()
+        if t in gas:
+            gx = gas[t]
+            big = gx > 1e-10
+            assert np.max(np.abs(xs[big] / gx[big] - 1)) < 2e-3, t
+            checked += 1
+        if t in surf:
+            gth = surf[t]
+            big = gth > 1e-10
+            assert np.max(np.abs(u[m.ng:][big] / gth[big] - 1)) < 1e-2, t
+            checked += 1
+    assert checked >= 6
+
+
+def test_analytic_jacobian_vs_fd(orc, gs_mech):
+    """Analytic Jacobian (new work) vs central differences of the oracle RHS."""
+    u0 = gs_u0(gs_mech)
+    u, _, _ = gs_mech.integrate(1173.0, 1.0, u0, 4e-3)   # post-ignition, radicals present
+    J = gs_mech.jac(1173.0, 1.0, u)
+    n = gs_mech.n
+    Jfd = np.zeros((n, n))
+    for j in range(n):
+        h = 1e-6 * max(abs(u[j]), 1e-12)
+        up, um = u.copy(), u.copy()
+        up[j] += h
+        um[j] -= h
+        Jfd[:, j] = (gs_mech.rhs(1173.0, 1.0, up)[0] - gs_mech.rhs(1173.0, 1.0, um)[0]) / (2 * h)
+    scale = np.abs(J).max(axis=1, keepdims=True) + 1e-300
+    assert np.max(np.abs(J - Jfd) / scale) < 2e-5
+
+
+def test_element_conservation(orc, gs_mech):
+    """Gas-phase rates conserve elements (per reaction stoichiometry)."""
+    u0 = gs_u0(gs_mech)
+    u, _, _ = gs_mech.integrate(1173.0, 1.0, u0, 4e-3)
+    m = orc.Mech(os.path.join(LIB, "grimech.dat"), TH)
+    du, p, x = m.rhs(1173.0, 1.0, u[:m.ng])
+    assert abs(du.sum()) <= 1e-12 * np.abs(du).sum()   # total mass
+
+
+def test_dq_and_analytic_solvers_agree(orc):
+    """CVODE with the DQ Jacobian (reference) and with the analytic Jacobian (engine) give the
+    same H2/O2 end state to the integration tolerance."""
+    m = orc.Mech(os.path.join(LIB, "h2o2.dat"), TH)
+    x = np.zeros(m.ng)
+    x[m.names.index("H2")], x[m.names.index("O2")], x[m.names.index("N2")] = 0.25, 0.25, 0.5
+    u0 = m.initial_state(1173.0, 1e5, x)
+    a, sa, _ = m.integrate(1173.0, 1.0, u0, 10.0, analytic_jac=True)
+    b, sb, _ = m.integrate(1173.0, 1.0, u0, 10.0, analytic_jac=False)
+    assert sa["status"] == 0 and sb["status"] == 0
+    big = b > 1e-8 * b.max()
+    assert np.max(np.abs(a[big] / b[big] - 1)) < 1e-4
