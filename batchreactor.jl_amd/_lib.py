@@ -6,7 +6,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(HERE, "libbrhip.so")
+LIBPATH = os.environ.get("BRHIP_LIB") or os.path.join(HERE, "libbrhip.so")
 
 dp = C.POINTER(C.c_double)
 ip = C.POINTER(C.c_int)
@@ -27,11 +27,15 @@ class MechDesc(C.Structure):
 
 class Opts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("max_steps", C.c_int), ("device", C.c_int),
-                ("hmax", C.c_double)]
+                ("hmax", C.c_double), ("trace_cap", C.c_int)]
+
+
+NSTAT = 14
 
 
 EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info",
-           "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_dev", "br_last_kernel_ms"]
+           "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_traced", "br_integrate_dev",
+           "br_last_kernel_ms", "br_debug_lu_solve"]
 
 _lib = None
 
@@ -54,10 +58,13 @@ def lib():
     L.br_rhs.argtypes = [vp, C.c_int, dp, dp, dp, dp]
     L.br_jacobian.argtypes = [vp, C.c_int, dp, dp, dp, dp]
     L.br_integrate.argtypes = [vp, C.c_int, dp, dp, dp, dp, C.POINTER(Opts), dp]
+    L.br_integrate_traced.argtypes = [vp, C.c_int, dp, dp, dp, dp, C.POINTER(Opts), dp, dp]
     L.br_integrate_dev.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.POINTER(Opts), vp, vp]
     L.br_last_kernel_ms.argtypes = [vp, dp]
+    L.br_debug_lu_solve.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, ip]
+    L.br_debug_lu_solve.restype = C.c_int
     for f in ("br_mech_create", "br_mech_destroy", "br_mech_info", "br_rates", "br_rhs", "br_jacobian",
-              "br_integrate", "br_integrate_dev", "br_last_kernel_ms"):
+              "br_integrate", "br_integrate_traced", "br_integrate_dev", "br_last_kernel_ms"):
         getattr(L, f).restype = C.c_int
     _lib = L
     return L

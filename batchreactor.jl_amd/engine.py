@@ -17,7 +17,8 @@ import numpy as np
 from . import _lib
 from .mechanism import Mechanism
 
-STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status")
+STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status", "cyc_total", "cyc_rhs",
+               "cyc_jac", "cyc_lu", "cyc_sol", "t_end")
 
 
 class Engine:
@@ -93,20 +94,30 @@ class Engine:
         _lib.check(_lib.lib().br_jacobian(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(J)))
         return J
 
-    def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000):
+    def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000, trace_cap=0):
+        """Integrate N reactors 0 -> tf. With trace_cap > 0 also returns the per-step rows
+        trace[N, trace_cap+1, n+4] = (t, h, q, p_last, u...)."""
         u = np.array(np.atleast_2d(u0), dtype=np.float64, order="C")
         N = u.shape[0]
         T, A, tf = self._arr(T, N), self._arr(Asv, N), self._arr(tf, N)
-        st = np.zeros((N, 8))
-        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0)
-        _lib.check(_lib.lib().br_integrate(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(tf),
-                                           C.byref(o), _lib.dptr(st)))
-        return u, {k: st[:, i] for i, k in enumerate(STAT_FIELDS)}
+        st = np.zeros((N, _lib.NSTAT))
+        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0, trace_cap)
+        L = _lib.lib()
+        if trace_cap > 0:
+            tr = np.zeros((N, trace_cap + 1, self.n + 4))
+            _lib.check(L.br_integrate_traced(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(tf),
+                                             C.byref(o), _lib.dptr(st), _lib.dptr(tr)))
+        else:
+            tr = None
+            _lib.check(L.br_integrate(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(tf),
+                                      C.byref(o), _lib.dptr(st)))
+        stats = {k: st[:, i] for i, k in enumerate(STAT_FIELDS)}
+        return (u, stats, tr) if trace_cap > 0 else (u, stats)
 
     def integrate_device(self, T_ptr, Asv_ptr, u_ptr, tf_ptr, stats_ptr, N, stream_ptr=None, rtol=1e-6,
                          atol=1e-10, max_steps=100000):
         """Device-resident variant: raw device pointers (e.g. torch tensor data_ptr())."""
-        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0)
+        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0, 0)
         _lib.check(_lib.lib().br_integrate_dev(self.h, N, C.c_void_p(T_ptr), C.c_void_p(Asv_ptr),
                                                C.c_void_p(u_ptr), C.c_void_p(tf_ptr), C.byref(o),
                                                C.c_void_p(stats_ptr), C.c_void_p(stream_ptr or 0)))

@@ -82,10 +82,15 @@ typedef struct br_opts {
     int max_steps;            /* default 100000 (Sundials.jl maxiters)             */
     int device;               /* HIP device ordinal for br_mech_create             */
     double hmax;              /* 0 = unbounded                                     */
+    int trace_cap;            /* br_integrate_traced: max accepted steps recorded  */
 } br_opts;
 
-typedef struct br_stats {     /* per reactor, counters as CVODE's                  */
+#define BR_NSTAT 14
+typedef struct br_stats {     /* per reactor; counters as CVODE's, then device cycles */
     double nsteps, nfe, nje, nsetups, nni, ncfn, netf, status;
+    double cyc_total;         /* wall clock ticks (100 MHz) for the whole reactor  */
+    double cyc_rhs, cyc_jac, cyc_lu, cyc_sol;  /* shader clocks in each phase      */
+    double t_end;             /* time reached                                      */
 } br_stats;
 
 int         br_version(void);
@@ -107,10 +112,21 @@ int br_jacobian(br_mech* m, int N, const double* T, const double* Asv, const dou
 int br_integrate(br_mech* m, int N, const double* T, const double* Asv, double* u /*in/out*/,
                  const double* tf, const br_opts* opts, br_stats* stats /*[N] or NULL*/);
 
+/* as br_integrate, and also records the state after every accepted step (the rows
+ * save_data writes, src/BatchReactor.jl:383-402): trace[N][trace_cap+1][n+4] with
+ * row = (t, h, q, p_last, u[0..n-1]); row 0 is t=0; unused rows are left as zeros.
+ * The last written row is the tstop row (t = tf). */
+int br_integrate_traced(br_mech* m, int N, const double* T, const double* Asv, double* u,
+                        const double* tf, const br_opts* opts, br_stats* stats, double* trace);
+
 /* device-buffer entry point: all pointers are device memory on m's device; `stream` is a
  * hipStream_t (NULL = default stream). Asynchronous: returns after the launch. */
 int br_integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv, double* du,
                      const double* dtf, const br_opts* opts, br_stats* dstats, void* stream);
+
+/* dense-solver check (tests): factor I - gamma_i*J_i with the engine's batched LU and solve
+ * x_i = (I - gamma_i J_i)^-1 b_i. J[N][n][n] row-major; fail[i] = 0 or (k+1) for a zero pivot. */
+int br_debug_lu_solve(int N, int n, const double* J, const double* gamma, const double* b, double* x, int* fail);
 
 /* timing helper for roofline accounting: duration (ms) of the last integrate kernel,
  * measured with HIP events on the stream it was launched on (after the stream syncs). */
