@@ -27,7 +27,7 @@ class MechDesc(C.Structure):
 
 class Opts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("max_steps", C.c_int), ("device", C.c_int),
-                ("hmax", C.c_double), ("trace_cap", C.c_int)]
+                ("hmax", C.c_double), ("trace_cap", C.c_int), ("unstable_factor", C.c_double)]
 
 
 NSTAT = 14

@@ -34,7 +34,7 @@ enum { FIRST_CALL = 0, PREV_CONV_FAIL = 1, PREV_ERR_FAIL = 2 };
 enum { NO_FAILURES = 0, FAIL_BAD_J = 1, FAIL_OTHER = 2 };
 
 struct KOpts {
-    double rtol, atol, hmax_inv;
+    double rtol, atol, hmax_inv, ufac;
     int max_steps, trace_cap;
 };
 
@@ -164,6 +164,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     wave_sync();
 
     z[0] = act ? U[(size_t)rid * n + lane] : 0.0;
+    const double ulimit = o.ufac * uni(wave_sum(act ? fabs(z[0]) : 0.0));
 
     auto F = [&](double yv) __attribute__((always_inline)) -> double {
         const unsigned long long c0 = clock64();
@@ -531,6 +532,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
         etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
         acor *= tq[2];
         nstloc++;
+        if (o.ufac > 0.0) {   // runaway state (br_opts.unstable_factor)
+            const double mx = uni(wave_max(act ? fabs(z[0]) : 0.0));
+            if (!(mx <= ulimit)) { status = BR_ERR_UNSTABLE; break; }
+        }
         if (trace && nst <= o.trace_cap) {   // per-step sample buffer (save_data rows)
             double* row = trace + ((size_t)rid * (o.trace_cap + 1) + nst) * (n + 4);
             if (lane == 0) { row[0] = tn; row[1] = h; row[2] = (double)q; row[3] = p_last; }
@@ -1015,6 +1020,7 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.max_steps = (opts && opts->max_steps > 0) ? opts->max_steps : 100000;
     o.hmax_inv = (opts && opts->hmax > 0) ? 1.0 / opts->hmax : 0.0;
     o.trace_cap = (opts && trace) ? opts->trace_cap : 0;
+    o.ufac = (opts && opts->unstable_factor != 0.0) ? opts->unstable_factor : 10.0;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipEventRecord(m->ev0, s));
     const int rpb = m->rpb;

@@ -116,7 +116,7 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(mech, T, Asv, U0, tf, dU.cpu().numpy(), args.cpu_seconds)
+        cpu, parity = cpu_baseline(mech, T, Asv, U0, tf, dU.cpu().numpy(), stats["status"], args.cpu_seconds)
 
     if rank == 0:
         total = N * world
@@ -142,7 +142,8 @@ def main():
                          "kernel": "k_integrate<64>", "kernel_ms": kernel_ms,
                          "algorithmic_flop_per_launch": flops},
             "cpu_baseline": cpu,
-            "solver": {"failed": nbad, "mean_steps": float(stats["nsteps"].mean()),
+            "solver": {"failed": nbad, "status_counts": {str(int(k)): int(np.sum(stats["status"] == k))
+                                                         for k in np.unique(stats["status"])}, "mean_steps": float(stats["nsteps"].mean()),
                        "mean_nfe": float(stats["nfe"].mean()), "mean_nje": float(stats["nje"].mean()),
                        "mean_nsetups": float(stats["nsetups"].mean())},
             "parity_vs_oracle_err": parity,
@@ -153,7 +154,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(mech, T, Asv, U0, tf, U_gpu, seconds):
+def cpu_baseline(mech, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
     """The C CPU oracle (CVODE restatement, analytic Jacobian, OpenMP over reactors) on a bounded
     sample of the same workload; also checks the GPU results of that sample against it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -175,8 +176,10 @@ def cpu_baseline(mech, T, Asv, U0, tf, U_gpu, seconds):
     t0 = time.perf_counter()
     Uo, sto, bad = om.integrate_batch(T[:k], Asv[:k], U0[:k], tf[:k], analytic_jac=True, nthreads=threads)
     dt = time.perf_counter() - t0
-    # parity metric of tests/test_gpu_parity.py: max |du| / (1e-4 |u| + 100 atol), pass <= 1
-    rel = float(np.max(np.abs(U_gpu[:k] - Uo) / (1e-4 * np.abs(Uo) + 1e-8)))
+    # parity metric of tests/test_gpu_parity.py: max |du| / (1e-4 |u| + 100 atol), pass <= 1,
+    # over the reactors both sides integrated successfully
+    ok = np.array([s["status"] == 0 for s in sto]) & (gpu_status[:k] == 0)
+    rel = float(np.max(np.abs(U_gpu[:k][ok] - Uo[ok]) / (1e-4 * np.abs(Uo[ok]) + 1e-8))) if ok.any() else None
     return ({"value": k / dt, "unit": "reactors/s", "cores": threads, "kind": "port",
              "sample": f"first {k} reactors of the same synthetic workload, C oracle (oracle/oracle.c, "
                        f"CVODE restatement, analytic Jacobian), OpenMP {threads} threads, {dt:.1f} s"}, rel)

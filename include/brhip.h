@@ -34,6 +34,7 @@ extern "C" {
 #define BR_ERR_MAXSTEPS  -1   /* CVODE CV_TOO_MUCH_WORK  */
 #define BR_ERR_ERRTEST   -3   /* CVODE CV_ERR_FAILURE     */
 #define BR_ERR_CONV      -4   /* CVODE CV_CONV_FAILURE    */
+#define BR_ERR_UNSTABLE  -7   /* runaway state (SciML ReturnCode.Unstable analogue; br_opts.unstable_factor) */
 #define BR_ERR_INPUT    -10
 #define BR_ERR_HIP      -20
 #define BR_ERR_UNSUPPORTED -30
@@ -83,6 +84,8 @@ typedef struct br_opts {
     int device;               /* HIP device ordinal for br_mech_create             */
     double hmax;              /* 0 = unbounded                                     */
     int trace_cap;            /* br_integrate_traced: max accepted steps recorded  */
+    double unstable_factor;   /* stop a reactor with BR_ERR_UNSTABLE once max_k |u_k| exceeds
+                                 factor * sum_k |u0_k| (0 = default 10, < 0 = never)     */
 } br_opts;
 
 #define BR_NSTAT 14

@@ -1340,6 +1340,8 @@ int orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf,
     if ((cv->tn + cv->h - cv->tstop) * cv->h > 0.0) cv->h = (cv->tstop - cv->tn) * (1.0 - 4.0 * cv->uround);
     cv->hscale = cv->h; cv->hprime = cv->h;
     for (int i = 0; i < n; ++i) cv->zn[1][i] *= cv->h;
+    double ufac = (o && o->unstable_factor != 0.0) ? o->unstable_factor : 10.0, uscale = 0.0;
+    for (int i = 0; i < n; ++i) uscale += fabs(u[i]);
     int status = 0;
     long nstloc = 0;
     for (;;) {
@@ -1348,6 +1350,11 @@ int orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf,
         int kf = cv_step(cv);
         if (kf) { status = kf; break; }
         nstloc++;
+        if (ufac > 0.0) {   /* runaway: a component far outside the physical range */
+            double mx = 0.0;
+            for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(cv->zn[0][i]));
+            if (!(mx <= ufac * uscale)) { status = -7; break; }
+        }
         double troundoff = FUZZ_FACTOR * cv->uround * (fabs(cv->tn) + fabs(cv->h));
         if (fabs(cv->tn - cv->tstop) <= troundoff) {
             get_dky(cv, cv->tstop, u);

@@ -42,11 +42,14 @@ typedef struct {
     int    analytic_jac;   /* 0 = CVODE DQ Jacobian (reference), 1 = analytic */
     int    max_steps;      /* Sundials.jl maxiters default 1e5 */
     double hmax;           /* 0 = inf */
+    double unstable_factor;/* abort (status -7) once max|u_k| > factor * sum|u0|; 0 = 10, <0 = off
+                              (DiffEq's unstable_check, see DESIGN.md "Failure detection") */
 } orc_opts;
 
 typedef struct {
     long nsteps, nfe, nje, nsetups, nni, ncfn, netf, nfeDQ;
-    int  status;           /* 0 ok, -1 too much work, -3 err fail, -4 conv fail, -6 LU fail */
+    int  status;           /* 0 ok, -1 too much work, -3 err fail, -4 conv fail, -6 LU fail,
+                              -7 unstable (runaway state) */
     int  qlast;
     double hlast, tcur;
 } orc_stats;

@@ -20,7 +20,7 @@ CONV_DOC_COVG = 4
 
 class Opts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("analytic_jac", C.c_int),
-                ("max_steps", C.c_int), ("hmax", C.c_double)]
+                ("max_steps", C.c_int), ("hmax", C.c_double), ("unstable_factor", C.c_double)]
 
 
 class Stats(C.Structure):

@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 }
 STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *tests* ]] && run pytest_gpu 900 python3 -m pytest tests -m gpu -x -q
+[[ $STEPS == *tests* ]] && run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 [[ $STEPS == *bench* ]] && run bench 900 python3 bench.py ${BENCH_ARGS:-}
-[[ $STEPS == *prof* ]] && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${PROF_ARGS:---n 20000 --steps 2 --warmup 1}
+[[ $STEPS == *prof* ]] && run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${PROF_ARGS:---n 20000 --steps 2 --warmup 1}
 echo done

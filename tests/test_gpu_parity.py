@@ -144,6 +144,11 @@ def _ignition_inputs(pm, case, N, seed):
 
 @pytest.mark.parametrize("case,N,tf", [("h2o2", 32, 10.0), ("gri", 8, 10.0), ("surf", 16, 10.0)])
 def test_integrate_parity(pkg, orc, gpu, case, N, tf):
+    """Default tolerances (rtol 1e-6, atol 1e-10, src/BatchReactor.jl:141,:210). Two CVODE runs that
+    differ only in rounding take different step sequences after ignition, and their end states then
+    agree only to the global error of the method (measured: oracle with analytic vs with DQ
+    Jacobian, the reference's own setting, differ by 1.4e-4 relative on this GRI sample). The bound is
+    1e-3 relative + 100 atol; test_integrate_parity_tight pins convergence to the same solution."""
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
     T, Asv, U0 = _ignition_inputs(pm, case, N, 5)
@@ -152,10 +157,31 @@ def test_integrate_parity(pkg, orc, gpu, case, N, tf):
     Uo, sto, bad = om.integrate_batch(T, Asv, U0, tf, analytic_jac=True, nthreads=4)
     assert bad == 0
     for i in range(N):
-        e = close_states(U[i], Uo[i])
+        e = close_states(U[i], Uo[i], rtol=1e-3)
         assert e <= 1.0, (case, i, e)
-        # same algorithm -> same step count up to rounding-induced path differences
-        assert abs(st["nsteps"][i] - sto[i]["nsteps"]) <= 0.25 * sto[i]["nsteps"] + 10
+    # same algorithm -> the same work up to rounding-induced path differences: after ignition
+    # single reactors can take quite different step sequences (both within tolerance), so the
+    # step count is compared over the batch
+    ng_, no_ = float(np.sum(st["nsteps"])), float(sum(s["nsteps"] for s in sto))
+    assert abs(ng_ - no_) <= 0.15 * no_, (ng_, no_)
+
+
+@pytest.mark.parametrize("case,N", [("h2o2", 16), ("gri", 4), ("surf", 8)])
+def test_integrate_parity_tight(pkg, orc, gpu, case, N):
+    """Tight tolerances (rtol 1e-10, atol 1e-16) on both sides: the two integrations converge to the
+    same trajectory, so the end states (tf = 1e-2 s, through ignition for the gas cases) must agree
+    to 1e-6 relative (absolute floor 1e-14 kg/m3)."""
+    pm, om = _mechs(pkg, orc, case)
+    eng = pkg.Engine(pm)
+    T, Asv, U0 = _ignition_inputs(pm, case, N, 6)
+    tf = 1e-2
+    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16)
+    assert np.all(st["status"] == 0)
+    for i in range(N):
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf, analytic_jac=True, rtol=1e-10, atol=1e-16)
+        assert so["status"] == 0
+        e = close_states(U[i], uo, rtol=1e-6, floor=1e-14)
+        assert e <= 1.0, (case, i, e)
 
 
 def test_integrate_edge_cases(pkg, orc, gpu):
