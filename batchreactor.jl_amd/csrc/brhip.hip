@@ -38,58 +38,531 @@ struct KOpts {
     int max_steps, trace_cap;
 };
 
-// per-reactor controller state (LDS)
+// ------------------------------------------------------------------------------------
+// per-reactor LDS block: [Ctl: CVODE's cv_mem scalars][Vec: per-lane vectors][Smem: rate work]
+//
+// The kernel keeps only the hot path inline (RHS, Jacobian, LU, solve). All step control lives
+// in two __noinline__ functions that read and write this block through address-space-3
+// pointers, so their register allocation is isolated from the hot path's (no spills there, and
+// the VGPR file stays free for the row-per-lane Newton matrix). Every lane writes the same
+// uniform value; reads go through readfirstlane, so branches on them are scalar.
+// ------------------------------------------------------------------------------------
 struct Ctl {
+    double p_last;
     double tau[QMAX + 2], tq[6], l[QMAX + 1];
-    double hprime, hscale, eta, etamax, gammap, crate, delp, acnrm, saved_tq5, p_last;
+    double tn, h, rl1, gamma, gamrat, gammap, crate, delp;
+    double hprime, hscale, eta, etamax, acnrm, saved_tq5, saved_t, tol;
+    double hg, hub, hlb, hnew, ulimit, tstop;
     int q, qprime, L, qwait;
-    int cnt[12];
-    int pstep[64];
+    int nst, nfe, nsetups, nje, nni, ncfn, netf, nstlp, nstlj;
+    int ncf, nef, nstloc, status, m_it, convfail, count1, phase;
+    int callSetup, jbad, jcur_nls, hnewOK, newj;
 };
 constexpr int CTL_BYTES = (sizeof(Ctl) + 15) / 16 * 16;
+enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, acor, ewt, tempv, y
+constexpr int VEC_BYTES = NVEC * WAVE * 8;
+typedef __attribute__((address_space(3))) Ctl LCtl;
+typedef __attribute__((address_space(3))) double LDbl;
 
-template <int K>
-__device__ __forceinline__ double getv(const double (&a)[K], int i) {
-    double v = 0.0;
-#pragma unroll
-    for (int t = 0; t < K; ++t) if (t == i) v = a[t];
-    return v;
-}
-template <int K>
-__device__ __forceinline__ void setv(double (&a)[K], int i, double v) {
-#pragma unroll
-    for (int t = 0; t < K; ++t) if (t == i) a[t] = v;
-}
-
-// LDS layout of a workgroup: [packed tables][reactor 0: Ctl | Smem | Nordsieck zs]...
-constexpr int ZS_VECS = QMAX + 4;   // z[0..QMAX], ewt, acor, tempv
 __host__ __device__ inline size_t reactor_bytes(const DevMech& M) {
-    return CTL_BYTES + reactor_doubles(M) * 8 + (size_t)ZS_VECS * WAVE * 8;
+    return CTL_BYTES + VEC_BYTES + (size_t)M.rblock_bytes;
 }
-struct LaneVec {   // component `lane` of vector j at p[j*64]
-    double* p;
-    __device__ __forceinline__ double& operator[](int j) const { return p[j * WAVE]; }
-};
-__host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return tab_bytes(M) + rpb * reactor_bytes(M); }
+__host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return M.img_bytes + rpb * reactor_bytes(M); }
+// per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn)
+__host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
+    return (size_t)2 * nmax * WAVE + (((size_t)2 * nrg + 63) / 64) * 64;
+}
 
 struct WaveCtx {
     int wave, lane, rid;
     Tab tb;
     char* rbase;   // this wave's reactor block
+    RView R;
 };
 __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rpb) {
     WaveCtx w;
-    w.wave = threadIdx.x >> 6;
+    w.wave = uni((int)(threadIdx.x >> 6));   // uniform per wave: scalar addressing of its reactor
     w.lane = threadIdx.x & 63;
     w.rid = blockIdx.x * rpb + w.wave;
-    stage_tables(M, reinterpret_cast<uint32_t*>(smem));
-    w.tb = tab_view(reinterpret_cast<const uint32_t*>(smem), M);
-    w.rbase = smem + tab_bytes(M) + (size_t)w.wave * reactor_bytes(M);
+    stage_tables(M, smem);
+    w.tb = tab_view(smem, M);
+    w.rbase = smem + M.img_bytes + (size_t)w.wave * reactor_bytes(M);
+    w.R = rview(w.rbase + CTL_BYTES + VEC_BYTES, M);
     return w;
 }
 
+// uniform loads from the LDS controller
+__device__ __forceinline__ double ud(const volatile LDbl& x) { return uni((double)x); }
+__device__ __forceinline__ int ui(const volatile __attribute__((address_space(3))) int& x) { return uni((int)x); }
+
+#ifndef BR_CTL_INLINE
+#define BR_CTL_INLINE __forceinline__
+#endif
+enum { PH_F0 = 0, PH_HIN = 1, PH_NEWTON = 2, PH_EF1 = 3 };
+// action codes returned by the controller to the hot loop
+enum { A_RHS = 0, A_SOLVE = 1, A_SETUP = 2, A_DONE = 3 };
+
+// wrms norm of a per-lane value with the weights in V[V_EWT]
+__device__ __forceinline__ double wrms_l(double v, double ewt, int lane, int n) {
+    const double t = (lane < n) ? v * ewt : 0.0;
+    return uni(sqrt(wave_sum(t * t) / n));
+}
+
+struct CtlArgs {   // per-launch constants the controller needs
+    double rtol, atol, hmax_inv, ufac;
+    int max_steps, trace_cap;
+    double* trace;
+    int rid, n;
+};
+
+// cvSet (BDF coefficients l[], tq[], gamma) for the current q, h, tau
+__device__ __forceinline__ void cv_set(LCtl* C) {
+    const int q = ui(C->q), qwait = ui(C->qwait), nst = ui(C->nst);
+    const double h = ud(C->h);
+    double lv[QMAX + 1] = {1.0, 1.0, 0.0, 0.0, 0.0, 0.0};
+    double tau[QMAX + 2];
+#pragma unroll
+    for (int i = 0; i < QMAX + 2; ++i) tau[i] = ud(C->tau[i]);
+    double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = h;
+    if (q > 1) {
+        for (int j = 2; j < q; ++j) {
+            hsum += tau[j - 1];
+            xi_inv = h / hsum;
+            alpha0 -= 1.0 / j;
+#pragma unroll
+            for (int i = QMAX; i >= 1; --i) if (i <= j) lv[i] += lv[i - 1] * xi_inv;
+        }
+        alpha0 -= 1.0 / q;
+        xistar_inv = -lv[1] - alpha0;
+        hsum += tau[q - 1];
+        xi_inv = h / hsum;
+        alpha0_hat = -lv[1] - xi_inv;
+#pragma unroll
+        for (int i = QMAX; i >= 1; --i) if (i <= q) lv[i] += lv[i - 1] * xistar_inv;
+    }
+#pragma unroll
+    for (int i = 0; i <= QMAX; ++i) C->l[i] = lv[i];
+    const double A1 = 1.0 - alpha0_hat + alpha0;
+    const double A2 = 1.0 + q * A1;
+    const double lq = lv[q];
+    const double tq2 = fabs(A1 / (alpha0 * A2));
+    C->tq[2] = tq2;
+    C->tq[5] = fabs(A2 * xistar_inv / (lq * xi_inv));
+    if (qwait == 1) {
+        if (q > 1) {
+            const double Cc = xistar_inv / lq;
+            const double A3 = alpha0 + 1.0 / q;
+            const double A4 = alpha0_hat + xi_inv;
+            const double Cpinv = (1.0 - A4 + A3) / A3;
+            C->tq[1] = fabs(Cc * Cpinv);
+        } else C->tq[1] = 1.0;
+        hsum += tau[q];
+        xi_inv = h / hsum;
+        const double A5 = alpha0 - (1.0 / (q + 1));
+        const double A6 = alpha0_hat - xi_inv;
+        const double Cppinv = (1.0 - A6 + A5) / A2;
+        C->tq[3] = fabs(Cppinv / (xi_inv * (q + 2) * A5));
+    }
+    C->tq[4] = CORTES / tq2;
+    const double rl1 = 1.0 / lv[1];
+    C->rl1 = rl1;
+    const double gamma = h * rl1;
+    C->gamma = gamma;
+    if (nst == 0) C->gammap = gamma;
+    C->gamrat = (nst > 0) ? gamma / ud(C->gammap) : 1.0;
+}
+
+// Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
+__device__ __forceinline__ void cv_rescale(LCtl* C, LDbl* V, int lane) {
+    const int q = ui(C->q);
+    const double eta = ud(C->eta);
+    double f = eta;
+    for (int j = 1; j <= q; ++j) { V[j * WAVE + lane] *= f; f *= eta; }
+    const double h = ud(C->hscale) * eta;
+    C->h = h; C->hscale = h;
+}
+// prediction (tn += h, Pascal triangle on z) and its inverse
+__device__ __forceinline__ void cv_predict(LCtl* C, LDbl* V, int lane) {
+    const int q = ui(C->q);
+    double tn = ud(C->tn) + ud(C->h);
+    const double tstop = ud(C->tstop);
+    if ((tn - tstop) * ud(C->h) > 0) tn = tstop;
+    C->tn = tn;
+    double z[QMAX + 1];
+#pragma unroll
+    for (int j = 0; j <= QMAX; ++j) z[j] = V[j * WAVE + lane];
+#pragma unroll
+    for (int k = 1; k <= QMAX; ++k)
+#pragma unroll
+        for (int j = QMAX; j >= k; --j)
+            if (j <= q && k <= q) z[j - 1] += z[j];
+#pragma unroll
+    for (int j = 0; j < QMAX; ++j) V[j * WAVE + lane] = z[j];
+}
+__device__ __forceinline__ void cv_restore(LCtl* C, LDbl* V, int lane) {
+    const int q = ui(C->q);
+    C->tn = ud(C->saved_t);
+    double z[QMAX + 1];
+#pragma unroll
+    for (int j = 0; j <= QMAX; ++j) z[j] = V[j * WAVE + lane];
+#pragma unroll
+    for (int k = 1; k <= QMAX; ++k)
+#pragma unroll
+        for (int j = QMAX; j >= k; --j)
+            if (j <= q && k <= q) z[j - 1] -= z[j];
+#pragma unroll
+    for (int j = 0; j < QMAX; ++j) V[j * WAVE + lane] = z[j];
+}
+// cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
+__device__ __forceinline__ void cv_adjust_order(LCtl* C, LDbl* V, int lane, int dq) {
+    const int q = ui(C->q);
+    if (q == 2 && dq != 1) return;
+    double lv[QMAX + 1] = {0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
+    const double hscale = ud(C->hscale);
+    if (dq == 1) {
+        double alpha1 = 1.0, prod = 1.0, xiold = 1.0, alpha0 = -1.0, hsum = hscale;
+        for (int j = 1; j < q; ++j) {
+            hsum += ud(C->tau[j + 1]);
+            const double xi = hsum / hscale;
+            prod *= xi;
+            alpha0 -= 1.0 / (j + 1);
+            alpha1 += 1.0 / xi;
+#pragma unroll
+            for (int i = QMAX; i >= 2; --i) if (i <= j + 2) lv[i] = lv[i] * xiold + lv[i - 1];
+            xiold = xi;
+        }
+        const double A1 = (-alpha0 - alpha1) / prod;
+        const double zL = A1 * V[QMAX * WAVE + lane];
+#pragma unroll
+        for (int j = 2; j <= QMAX; ++j) if (j <= q) V[j * WAVE + lane] += lv[j] * zL;
+        V[(q + 1) * WAVE + lane] = zL;
+    } else {
+        double hsum = 0.0;
+        for (int j = 1; j <= q - 2; ++j) {
+            hsum += ud(C->tau[j]);
+            const double xi = hsum / hscale;
+#pragma unroll
+            for (int i = QMAX; i >= 2; --i) if (i <= j + 2) lv[i] = lv[i] * xi + lv[i - 1];
+        }
+        const double zq = V[q * WAVE + lane];
+#pragma unroll
+        for (int j = 2; j < QMAX; ++j) if (j < q) V[j * WAVE + lane] -= lv[j] * zq;
+    }
+}
+__device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, int step, double t, double v) {
+    if (a.trace && step <= a.trace_cap) {
+        double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + step) * (a.n + 4);
+        if (lane == 0) { row[0] = t; row[1] = ud(C->h); row[2] = (double)ui(C->q); row[3] = ud(C->p_last); }
+        if (lane < a.n) row[4 + lane] = v;
+    }
+}
+// one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
+__device__ __forceinline__ void begin_attempt(LCtl* C, LDbl* V, int lane, int nflag) {
+    cv_predict(C, V, lane);
+    cv_set(C);
+    const int nst = ui(C->nst);
+    C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
+    C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
+                   (nst >= ui(C->nstlp) + MSBP) || (fabs(ud(C->gamrat) - 1.0) > DGMAX);
+    V[V_ACOR * WAVE + lane] = 0.0;
+    C->tol = ud(C->tq[4]);
+    C->jbad = 0;
+    C->jcur_nls = 0;
+    C->m_it = 0;
+    V[V_Y * WAVE + lane] = V[lane];   // y = z0
+}
+__device__ __forceinline__ void begin_step(LCtl* C, LDbl* V, int lane, const CtlArgs& a) {
+    const double z0 = V[lane];
+    V[V_EWT * WAVE + lane] = (lane < a.n) ? 1.0 / (a.rtol * fabs(z0) + a.atol) : 1.0;
+    C->saved_t = ud(C->tn);
+    C->ncf = 0; C->nef = 0;
+    if ((ui(C->nst) > 0) && (ud(C->hprime) != ud(C->h))) {
+        const int qp = ui(C->qprime), q = ui(C->q);
+        if (qp != q) {
+            cv_adjust_order(C, V, lane, qp - q);
+            C->q = qp; C->L = qp + 1; C->qwait = qp + 1;
+        }
+        cv_rescale(C, V, lane);
+    }
+    begin_attempt(C, V, lane, FIRST_CALL);
+}
+
+// Controller, part 1: after the RHS value f = F(y) of this lane is known.
+// Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
+// A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, const CtlArgs a, double* rhs_out) {
+    const int n = a.n;
+    const bool act = lane < n;
+    C->nfe = ui(C->nfe) + 1;
+    const int phase = ui(C->phase);
+    const double z0 = V[lane];
+    if (phase == PH_NEWTON) {
+        const double acor = V[V_ACOR * WAVE + lane];
+        const double delta = (ud(C->rl1) * V[WAVE + lane] + acor) - ud(C->gamma) * f;   // cvNlsResidual
+        *rhs_out = -delta;
+        if (ui(C->m_it) == 0 && ui(C->callSetup)) {          // cvLsSetup decision
+            const int nst = ui(C->nst);
+            const double dgamma = fabs(ud(C->gamma) / ud(C->gammap) - 1.0);
+            const int cf = ui(C->jbad) ? FAIL_BAD_J : ui(C->convfail);
+            const int newj = (nst == 0) || (nst > ui(C->nstlj) + LS_MSBJ) || ((cf == FAIL_BAD_J) && (dgamma < LS_DGMAX)) ||
+                             (cf == FAIL_OTHER);
+            C->newj = newj;
+            if (newj) { C->nje = ui(C->nje) + 1; C->nstlj = nst; }
+            C->nsetups = ui(C->nsetups) + 1;
+            C->jcur_nls = newj;
+            C->gamrat = 1.0; C->gammap = ud(C->gamma); C->crate = 1.0; C->nstlp = nst;
+            return A_SETUP;
+        }
+        return A_SOLVE;
+    }
+    double h = 0.0;
+    if (phase == PH_EF1) {   // restart at order 1 after repeated error-test failures
+        V[WAVE + lane] = ud(C->h) * f;
+        begin_attempt(C, V, lane, PREV_ERR_FAIL);
+        C->phase = PH_NEWTON;
+        return A_RHS;
+    }
+    const double z1in = (phase == PH_F0) ? f : V[WAVE + lane];
+    const double ewt = V[V_EWT * WAVE + lane];
+    if (phase == PH_F0) {
+        V[WAVE + lane] = f;
+        const double tn = ud(C->tn), tstop = ud(C->tstop);
+        const double tdist = fabs(tstop - tn);
+        const double tround = UROUND * fmax(fabs(tn), fabs(tstop));
+        const double hlb = HLB_FACTOR * tround;
+        const double ratio = act ? fabs(f) / (HUB_FACTOR * fabs(z0) + 1.0 / ewt) : 0.0;
+        const double hub_inv = uni(wave_max(ratio));
+        double hub = HUB_FACTOR * tdist;
+        if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
+        const double hg = sqrt(hlb * hub);
+        C->hlb = hlb; C->hub = hub; C->hg = hg;
+        if (hub < hlb) {
+            h = hg;
+        } else {
+            C->count1 = 1; C->hnewOK = 0; C->hnew = hg;
+            V[V_Y * WAVE + lane] = hg * f + z0;
+            C->phase = PH_HIN;
+            return A_RHS;
+        }
+    } else {                 // PH_HIN (cvYddNorm + the cvHin iteration)
+        double hg = ud(C->hg);
+        const double hub = ud(C->hub), hlb = ud(C->hlb);
+        const double tempv = (f - z1in) * (1.0 / hg);
+        const double yddnrm = wrms_l(tempv, ewt, lane, n);
+        const int count1 = ui(C->count1);
+        double hnew;
+        if (ui(C->hnewOK) || count1 == MAX_ITERS) {
+            hnew = hg;
+        } else {
+            hnew = (yddnrm * hub * hub > 2.0) ? sqrt(2.0 / yddnrm) : sqrt(hg * hub);
+            const double hrat = hnew / hg;
+            int ok = 0;
+            if ((hrat > 0.5) && (hrat < 2.0)) ok = 1;
+            if ((count1 > 1) && (hrat > 2.0)) { hnew = hg; ok = 1; }
+            C->hnewOK = ok;
+            hg = hnew;
+            C->hg = hg;
+            C->count1 = count1 + 1;
+            V[V_Y * WAVE + lane] = hg * z1in + z0;
+            return A_RHS;
+        }
+        double h0 = H_BIAS * hnew;
+        if (h0 < hlb) h0 = hlb;
+        if (h0 > hub) h0 = hub;
+        h = h0;
+    }
+    // ---- first step size known
+    if (a.hmax_inv > 0) { const double rh = fabs(h) * a.hmax_inv; if (rh > 1.0) h /= rh; }
+    const double tn = ud(C->tn), tstop = ud(C->tstop);
+    if ((tn + h - tstop) * h > 0.0) h = (tstop - tn) * (1.0 - 4.0 * UROUND);
+    C->h = h; C->hscale = h; C->hprime = h;
+    trace_row(C, a, lane, 0, 0.0, z0);
+    V[WAVE + lane] *= h;
+    if (a.max_steps <= 0) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
+    begin_step(C, V, lane, a);
+    C->phase = PH_NEWTON;
+    return A_RHS;
+}
+
+// Controller, part 2: after the linear solve (delta = this lane's Newton correction) or after
+// an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
+// cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double delta, int lu_fail, const CtlArgs a) {
+    const int n = a.n;
+    const bool act = lane < n;
+    const double ewt = V[V_EWT * WAVE + lane];
+    int nls;                                                   // 0 converged, else failure
+    if (lu_fail) {
+        nls = 2;
+    } else {
+        C->nni = ui(C->nni) + 1;
+        const double gamrat = ud(C->gamrat);
+        if (gamrat != 1.0) delta *= 2.0 / (1.0 + gamrat);
+        const double acor = V[V_ACOR * WAVE + lane] + delta;
+        V[V_ACOR * WAVE + lane] = acor;
+        const double del = wrms_l(delta, ewt, lane, n);     // cvNlsConvTest
+        const int m = ui(C->m_it);
+        double crate = ud(C->crate);
+        const double delp = ud(C->delp);
+        if (m > 0) { crate = fmax(CRDOWN * crate, del / delp); C->crate = crate; }
+        const double dcon = del * fmin(1.0, crate) / ud(C->tol);
+        if (dcon <= 1.0) {
+            C->acnrm = (m == 0) ? del : wrms_l(acor, ewt, lane, n);
+            nls = 0;
+        } else {
+            bool fail = (m >= 1) && (del > RDIV * delp);
+            if (!fail) {
+                C->delp = del;
+                C->m_it = m + 1;
+                if (m + 1 >= NLS_MAXCOR) fail = true;
+            }
+            if (!fail) {
+                V[V_Y * WAVE + lane] = V[lane] + acor;
+                return A_RHS;
+            }
+            if (!ui(C->jcur_nls)) {                          // retry with a fresh Jacobian
+                C->callSetup = 1; C->jbad = 1; C->m_it = 0;
+                V[V_ACOR * WAVE + lane] = 0.0;
+                V[V_Y * WAVE + lane] = V[lane];
+                return A_RHS;
+            }
+            nls = 1;
+        }
+    }
+    if (nls != 0) {                                          // cvHandleNFlag
+        C->ncfn = ui(C->ncfn) + 1;
+        cv_restore(C, V, lane);
+        const int ncf = ui(C->ncf) + 1;
+        C->ncf = ncf;
+        C->etamax = 1.0;
+        if (ncf == MXNCF) { C->status = BR_ERR_CONV; return A_DONE; }
+        C->eta = ETACF;
+        cv_rescale(C, V, lane);
+        begin_attempt(C, V, lane, PREV_CONV_FAIL);
+        return A_RHS;
+    }
+    // ---- cvDoErrorTest
+    const double dsm = ud(C->acnrm) * ud(C->tq[2]);
+    const int q = ui(C->q);
+    if (dsm > 1.0) {
+        const int nef = ui(C->nef) + 1;
+        C->nef = nef; C->netf = ui(C->netf) + 1;
+        cv_restore(C, V, lane);
+        if (nef == MXNEF) { C->status = BR_ERR_ERRTEST; return A_DONE; }
+        C->etamax = 1.0;
+        if (nef <= MXNEF1) {
+            double eta = 1.0 / (pow(BIAS2 * dsm, 1.0 / ui(C->L)) + ADDON);
+            eta = fmax(ETAMIN, eta);
+            if (nef >= SMALL_NEF) eta = fmin(eta, ETAMXF);
+            C->eta = eta;
+            cv_rescale(C, V, lane);
+            begin_attempt(C, V, lane, PREV_ERR_FAIL);
+            return A_RHS;
+        }
+        if (q > 1) {
+            C->eta = ETAMIN;
+            cv_adjust_order(C, V, lane, -1);
+            C->L = q; C->q = q - 1; C->qwait = q;
+            cv_rescale(C, V, lane);
+            begin_attempt(C, V, lane, PREV_ERR_FAIL);
+            return A_RHS;
+        }
+        C->eta = ETAMIN;
+        const double h = ud(C->h) * ETAMIN;
+        C->h = h; C->hscale = h; C->qwait = LONG_WAIT;
+        V[V_Y * WAVE + lane] = V[lane];
+        C->phase = PH_EF1;
+        return A_RHS;
+    }
+    // ---- cvCompleteStep
+    const int nst = ui(C->nst) + 1;
+    C->nst = nst;
+    const double h = ud(C->h);
+    for (int i = q; i >= 2; --i) C->tau[i] = ud(C->tau[i - 1]);
+    if ((q == 1) && (nst > 1)) C->tau[2] = ud(C->tau[1]);
+    C->tau[1] = h;
+    const double acor = V[V_ACOR * WAVE + lane];
+#pragma unroll
+    for (int j = 0; j <= QMAX; ++j) if (j <= q) V[j * WAVE + lane] += ud(C->l[j]) * acor;
+    int qwait = ui(C->qwait) - 1;
+    if ((qwait == 1) && (q != QMAX)) { V[QMAX * WAVE + lane] = acor; C->saved_tq5 = ud(C->tq[5]); }
+    // ---- cvPrepareNextStep
+    double eta = 1.0, hprime = h;
+    int qprime = q;
+    const double etamax = ud(C->etamax);
+    if (etamax == 1.0) {
+        qwait = qwait > 2 ? qwait : 2;
+    } else {
+        const int L = ui(C->L);
+        const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / L) + ADDON);
+        if (qwait != 0) { eta = etaq; }
+        else {
+            qwait = 2;
+            double etaqm1 = 0.0, etaqp1 = 0.0;
+            if (q > 1) {
+                const double ddn = wrms_l(V[q * WAVE + lane], ewt, lane, n) * ud(C->tq[1]);
+                etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / q) + ADDON);
+            }
+            const double saved_tq5 = ud(C->saved_tq5);
+            if (q != QMAX && saved_tq5 != 0.0) {
+                const double cquot = (ud(C->tq[5]) / saved_tq5) * pow(h / ud(C->tau[2]), (double)L);
+                const double tempv = acor - cquot * V[QMAX * WAVE + lane];
+                const double dup = wrms_l(tempv, ewt, lane, n) * ud(C->tq[3]);
+                etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (L + 1)) + ADDON);
+            }
+            const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
+            if (etam < THRESH) { eta = 1.0; }
+            else if (etam == etaq) { eta = etaq; }
+            else if (etam == etaqm1) { eta = etaqm1; qprime = q - 1; }
+            else { eta = etaqp1; qprime = q + 1; V[QMAX * WAVE + lane] = acor; }
+        }
+        if (eta < THRESH) { eta = 1.0; hprime = h; }                // cvSetEta
+        else {
+            eta = fmin(eta, etamax);
+            eta /= fmax(1.0, fabs(h) * a.hmax_inv * eta);
+            hprime = h * eta;
+        }
+    }
+    C->qwait = qwait;
+    C->etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+    V[V_ACOR * WAVE + lane] = acor * ud(C->tq[2]);
+    const int nstloc = ui(C->nstloc) + 1;
+    C->nstloc = nstloc;
+    const double tn = ud(C->tn);
+    const double z0 = V[lane];
+    C->eta = eta; C->hprime = hprime; C->qprime = qprime;
+    trace_row(C, a, lane, nst, tn, z0);
+    if (a.ufac > 0.0) {                                      // runaway state (br_opts.unstable_factor)
+        const double mx = uni(wave_max(act ? fabs(z0) : 0.0));
+        if (!(mx <= ud(C->ulimit))) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
+    }
+    // CVode ONE_STEP + tstop handling
+    const double tstop = ud(C->tstop);
+    const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
+    if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
+        const double sk = (tstop - tn) / h;
+        double yv = V[q * WAVE + lane];
+        for (int j = q - 1; j >= 0; --j) yv = V[j * WAVE + lane] + sk * yv;
+        V[V_Y * WAVE + lane] = yv;
+        if (a.trace && nst <= a.trace_cap) {
+            double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + nst) * (n + 4);
+            if (lane == 0) row[0] = tstop;
+            if (act) row[4 + lane] = yv;
+        }
+        return A_DONE;
+    }
+    if ((tn + hprime - tstop) * h > 0.0) {
+        hprime = (tstop - tn) * (1.0 - 4.0 * UROUND);
+        C->hprime = hprime;
+        C->eta = hprime / h;
+    }
+    if (nstloc >= a.max_steps) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
+    begin_step(C, V, lane, a);
+    return A_RHS;
+}
+
 // ------------------------------------------------------------------------------------
-// the integrator: one reactor per 64-lane workgroup
+// the integrator kernel: one reactor per 64-lane wavefront, `rpb` reactors per workgroup
 // ------------------------------------------------------------------------------------
 #ifndef BR_WPE
 #define BR_WPE 2
@@ -105,474 +578,106 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     if (rid >= N) return;
     const int lane = W.lane;
     const Tab& tb = W.tb;
-    double* smem = reinterpret_cast<double*>(W.rbase);
+    const size_t roff = (size_t)(W.rbase - smem_raw);
+    LCtl* C = (LCtl*)(smem_raw + roff);
+    LDbl* V = (LDbl*)(smem_raw + roff + CTL_BYTES);
+    const RView& S = W.R;
     const int n = M.n;
     const bool act = lane < n;
-    Smem S = carve(smem + CTL_BYTES / 8, M);
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
-    const double tstop = tfv[rid];
-    const double Mk = act ? M.molwt[lane] : 1.0;
-    double* Jsave = Jws + (size_t)rid * 2 * NMAX * WAVE;   // J, then the LU factors
+    double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
     double* LUsave = Jsave + NMAX * WAVE;
+    double* jscr = LUsave + NMAX * WAVE;
+    CtlArgs a;
+    a.rtol = o.rtol; a.atol = o.atol; a.hmax_inv = o.hmax_inv; a.ufac = o.ufac;
+    a.max_steps = o.max_steps; a.trace_cap = o.trace_cap; a.trace = trace; a.rid = rid; a.n = n;
 
     init_tconst(M, tb, S, T, lane);
 
-    // Nordsieck history and long-lived work vectors (this lane's component) live in the
-    // reactor's LDS block: zs[j*64 + lane]; y/ftemp/delta stay in registers
-    double* zs = smem + CTL_BYTES / 8 + reactor_doubles(M);
-    const LaneVec z{zs + lane};
-    double& ewt = zs[(QMAX + 1) * WAVE + lane];
-    double& acor = zs[(QMAX + 2) * WAVE + lane];
-    double& tempv = zs[(QMAX + 3) * WAVE + lane];
+    // ---- CVodeInit
+    const double u0 = act ? U[(size_t)rid * n + lane] : 0.0;
 #pragma unroll
-    for (int j = 0; j <= QMAX; ++j) z[j] = 0.0;
-    ewt = 1.0; acor = 0.0; tempv = 0.0;
-    double y = 0.0, ftemp = 0.0, delta = 0.0;
-    int pstep = -1;
-    // uniform controller state: kept in LDS (one copy per reactor) to free VGPRs for the
-    // row-per-lane Newton matrix; every lane reads/writes the same values.
-    Ctl& C = *reinterpret_cast<Ctl*>(smem);
-    double (&tau)[QMAX + 2] = C.tau;
-    double (&tq)[6] = C.tq;
-    double (&l)[QMAX + 1] = C.l;
+    for (int j = 0; j < NVEC; ++j) V[j * WAVE + lane] = 0.0;
+    V[lane] = u0;
+    V[V_Y * WAVE + lane] = u0;
+    V[V_EWT * WAVE + lane] = act ? 1.0 / (o.rtol * fabs(u0) + o.atol) : 1.0;
 #pragma unroll
-    for (int i = 0; i < QMAX + 2; ++i) tau[i] = 0.0;
+    for (int i = 0; i < QMAX + 2; ++i) C->tau[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) tq[i] = 0.0;
+    for (int i = 0; i < 6; ++i) C->tq[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i <= QMAX; ++i) l[i] = 0.0;
-    double tn = 0.0, h = 0.0, rl1 = 0.0, gamma = 0.0, gamrat = 1.0;
-    double& hprime = C.hprime; double& hscale = C.hscale; double& eta = C.eta; double& etamax = C.etamax;
-    double& gammap = C.gammap; double& crate = C.crate; double& delp = C.delp; double& acnrm = C.acnrm;
-    double& saved_tq5 = C.saved_tq5;
-    hprime = 0.0; hscale = 0.0; eta = 1.0; etamax = ETAMX1; gammap = 0.0; crate = 1.0; delp = 0.0; acnrm = 0.0;
-    saved_tq5 = 0.0;
-    int& q = C.q; int& qprime = C.qprime; int& L = C.L; int& qwait = C.qwait;
-    q = 1; qprime = 1; L = 2; qwait = 2;
-    int& nst = C.cnt[0]; int& nfe = C.cnt[1]; int& nsetups = C.cnt[2]; int& nje = C.cnt[3]; int& nni = C.cnt[4];
-    int& ncfn = C.cnt[5]; int& netf = C.cnt[6]; int& nstlp = C.cnt[7]; int& nstlj = C.cnt[8];
-    int& jcur = C.cnt[9];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) C.cnt[i] = 0;
-    double& p_last = C.p_last;
-    const double hmin = 0.0;
-    // phase cycle counters (lane 0 accumulates)
+    for (int i = 0; i <= QMAX; ++i) C->l[i] = 0.0;
+    C->tn = 0.0; C->h = 0.0; C->rl1 = 0.0; C->gamma = 0.0; C->gamrat = 1.0; C->gammap = 0.0; C->crate = 1.0;
+    C->delp = 0.0; C->hprime = 0.0; C->hscale = 0.0; C->eta = 1.0; C->etamax = ETAMX1; C->acnrm = 0.0;
+    C->saved_tq5 = 0.0; C->saved_t = 0.0; C->tol = 0.0; C->hg = 0.0; C->hub = 0.0; C->hlb = 0.0; C->hnew = 0.0;
+    C->tstop = tfv[rid];
+    C->ulimit = o.ufac * uni(wave_sum(act ? fabs(u0) : 0.0));
+    C->q = 1; C->qprime = 1; C->L = 2; C->qwait = 2;
+    C->nst = 0; C->nfe = 0; C->nsetups = 0; C->nje = 0; C->nni = 0; C->ncfn = 0; C->netf = 0; C->nstlp = 0;
+    C->nstlj = 0; C->ncf = 0; C->nef = 0; C->nstloc = 0; C->status = 0; C->m_it = 0; C->convfail = 0;
+    C->count1 = 0; C->phase = PH_F0; C->callSetup = 0; C->jbad = 0; C->jcur_nls = 0; C->hnewOK = 0; C->newj = 0;
+    C->p_last = 0.0;
+
     unsigned long long cyc_rhs = 0, cyc_jac = 0, cyc_lu = 0, cyc_sol = 0;
     const unsigned long long cyc0 = wall_clock64();
-    wave_sync();
-
-    z[0] = act ? U[(size_t)rid * n + lane] : 0.0;
-    const double ulimit = o.ufac * uni(wave_sum(act ? fabs(z[0]) : 0.0));
-
-    auto F = [&](double yv) __attribute__((always_inline)) -> double {
-        const unsigned long long c0 = clock64();
-        const double r = rhs(M, tb, S, T, Asv, Asv_th, yv, lane, Mk, &p_last);
-        cyc_rhs += clock64() - c0;
-        return r;
-    };
-    auto wrms = [&](double v) __attribute__((always_inline)) -> double {
-        const double t = act ? v * ewt : 0.0;
-        return uni(sqrt(wave_sum(t * t) / n));
-    };
-    auto set_ewt = [&]() __attribute__((always_inline)) { ewt = act ? 1.0 / (o.rtol * fabs(z[0]) + o.atol) : 1.0; };
-
-    auto rescale = [&]() __attribute__((always_inline)) {
-        double factor = eta;
-#pragma unroll
-        for (int j = 1; j <= QMAX; ++j) if (j <= q) { z[j] *= factor; factor *= eta; }
-        h = hscale * eta; hscale = h;
-    };
-    auto predict = [&]() __attribute__((always_inline)) {
-        tn += h;
-        if ((tn - tstop) * h > 0) tn = tstop;
-#pragma unroll
-        for (int k = 1; k <= QMAX; ++k)
-#pragma unroll
-            for (int j = QMAX; j >= k; --j)
-                if (j <= q && k <= q) z[j - 1] += z[j];
-    };
-    auto restore = [&](double saved_t) __attribute__((always_inline)) {
-        tn = saved_t;
-#pragma unroll
-        for (int k = 1; k <= QMAX; ++k)
-#pragma unroll
-            for (int j = QMAX; j >= k; --j)
-                if (j <= q && k <= q) z[j - 1] -= z[j];
-    };
-    auto cvset = [&]() __attribute__((always_inline)) {
-        double xi_inv = 1.0, xistar_inv = 1.0;
-        l[0] = 1.0; l[1] = 1.0;
-#pragma unroll
-        for (int i = 2; i <= QMAX; ++i) l[i] = 0.0;
-        double alpha0 = -1.0, alpha0_hat = -1.0, hsum = h;
-        if (q > 1) {
-#pragma unroll
-            for (int j = 2; j < QMAX; ++j) {
-                if (j < q) {
-                    hsum += tau[j - 1];
-                    xi_inv = h / hsum;
-                    alpha0 -= 1.0 / j;
-#pragma unroll
-                    for (int i = QMAX; i >= 1; --i) if (i <= j) l[i] += l[i - 1] * xi_inv;
-                }
-            }
-            alpha0 -= 1.0 / q;
-            xistar_inv = -l[1] - alpha0;
-            hsum += getv(tau, q - 1);
-            xi_inv = h / hsum;
-            alpha0_hat = -l[1] - xi_inv;
-#pragma unroll
-            for (int i = QMAX; i >= 1; --i) if (i <= q) l[i] += l[i - 1] * xistar_inv;
-        }
-        // cvSetTqBDF
-        const double A1 = 1.0 - alpha0_hat + alpha0;
-        const double A2 = 1.0 + q * A1;
-        const double lq = getv(l, q);
-        tq[2] = fabs(A1 / (alpha0 * A2));
-        tq[5] = fabs(A2 * xistar_inv / (lq * xi_inv));
-        if (qwait == 1) {
-            if (q > 1) {
-                const double C = xistar_inv / lq;
-                const double A3 = alpha0 + 1.0 / q;
-                const double A4 = alpha0_hat + xi_inv;
-                const double Cpinv = (1.0 - A4 + A3) / A3;
-                tq[1] = fabs(C * Cpinv);
-            } else tq[1] = 1.0;
-            hsum += getv(tau, q);
-            xi_inv = h / hsum;
-            const double A5 = alpha0 - (1.0 / (q + 1));
-            const double A6 = alpha0_hat - xi_inv;
-            const double Cppinv = (1.0 - A6 + A5) / A2;
-            tq[3] = fabs(Cppinv / (xi_inv * (q + 2) * A5));
-        }
-        tq[4] = CORTES / tq[2];
-        rl1 = 1.0 / l[1];
-        gamma = h * rl1;
-        if (nst == 0) gammap = gamma;
-        gamrat = (nst > 0) ? gamma / gammap : 1.0;
-    };
-    auto adjust_order = [&](int dq) __attribute__((always_inline)) {
-        if (q == 2 && dq != 1) return;
-        if (dq == 1) {  // cvIncreaseBDF
-#pragma unroll
-            for (int i = 0; i <= QMAX; ++i) l[i] = 0.0;
-            l[2] = 1.0;
-            double alpha1 = 1.0, prod = 1.0, xiold = 1.0, alpha0 = -1.0, hsum = hscale;
-            if (q > 1) {
-#pragma unroll
-                for (int j = 1; j < QMAX; ++j) {
-                    if (j < q) {
-                        hsum += tau[j + 1];
-                        const double xi = hsum / hscale;
-                        prod *= xi;
-                        alpha0 -= 1.0 / (j + 1);
-                        alpha1 += 1.0 / xi;
-#pragma unroll
-                        for (int i = QMAX; i >= 2; --i) if (i <= j + 2) l[i] = l[i] * xiold + l[i - 1];
-                        xiold = xi;
-                    }
-                }
-            }
-            const double A1 = (-alpha0 - alpha1) / prod;
-            const double zL = A1 * z[QMAX];   // zn[L] = A1 * zn[indx_acor], indx_acor = qmax
-#pragma unroll
-            for (int j = 2; j <= QMAX; ++j) if (j <= q) z[j] += l[j] * zL;
-#pragma unroll
-            for (int j = 1; j <= QMAX; ++j) if (j == q + 1) z[j] = zL;
-        } else {        // cvDecreaseBDF
-#pragma unroll
-            for (int i = 0; i <= QMAX; ++i) l[i] = 0.0;
-            l[2] = 1.0;
-            double hsum = 0.0;
-#pragma unroll
-            for (int j = 1; j <= QMAX - 2; ++j) {
-                if (j <= q - 2) {
-                    hsum += tau[j];
-                    const double xi = hsum / hscale;
-#pragma unroll
-                    for (int i = QMAX; i >= 2; --i) if (i <= j + 2) l[i] = l[i] * xi + l[i - 1];
-                }
-            }
-            double zq = 0.0;
-#pragma unroll
-            for (int j = 0; j <= QMAX; ++j) if (j == q) zq = z[j];
-#pragma unroll
-            for (int j = 2; j < QMAX; ++j) if (j < q) z[j] -= l[j] * zq;
-        }
-    };
-    // cvLsSetup: A = I - gamma*J (J fresh or saved) and factor it
-    auto lsetup = [&](int convfail) __attribute__((always_inline)) -> int {
-        const double dgamma = fabs(gamma / gammap - 1.0);
-        const bool jbad = (nst == 0) || (nst > nstlj + LS_MSBJ) || ((convfail == FAIL_BAD_J) && (dgamma < LS_DGMAX)) ||
-                          (convfail == FAIL_OTHER);
-        if (!jbad) {
-            jcur = 0;
-        } else {
-            jcur = 1; nje++; nstlj = nst;
-            const unsigned long long c0 = clock64();
-            jacobian(M, tb, S, T, Asv, Asv_th, y, lane, Mk, Jsave);
-            cyc_jac += clock64() - c0;
-        }
-        const unsigned long long c1 = clock64();
-        const int rc = lu_factor_mem<NMAX>(Jsave, LUsave, gamma, n, lane, &C.pstep[lane]);
-        pstep = C.pstep[lane];
-        cyc_lu += clock64() - c1;
-        return rc;
-    };
-    // cvNls with SUNNonlinSol_Newton semantics
-    auto nls = [&](int nflag) __attribute__((always_inline)) -> int {
-        const int convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
-        bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
-                         (nst >= nstlp + MSBP) || (fabs(gamrat - 1.0) > DGMAX);
-        acor = 0.0;
-        const double tol = tq[4];
-        bool jbad = false;
-        int jc = 0;
-        int m = 0;
-        for (;;) {
-            y = z[0] + acor;
-            ftemp = F(y);
-            nfe++;
-            delta = (rl1 * z[1] + acor) - gamma * ftemp;
-            if (m == 0 && callSetup) {
-                const int lr = lsetup(jbad ? FAIL_BAD_J : convfail);
-                nsetups++;
-                jc = jcur;
-                gamrat = 1.0; gammap = gamma; crate = 1.0; nstlp = nst;
-                if (lr) { y = z[0] + acor; return 2; }
-            }
-            nni++;
-            delta = -delta;
-            {
-                const unsigned long long c0 = clock64();
-                delta = lu_solve_mem<NMAX>(LUsave, n, lane, pstep, delta);
-                cyc_sol += clock64() - c0;
-            }
-            if (gamrat != 1.0) delta *= 2.0 / (1.0 + gamrat);
-            acor += delta;
-            const double del = wrms(delta);
-            if (m > 0) crate = fmax(CRDOWN * crate, del / delp);
-            const double dcon = del * fmin(1.0, crate) / tol;
-            if (dcon <= 1.0) {
-                acnrm = (m == 0) ? del : wrms(acor);
-                y = z[0] + acor;
-                jcur = 0;
-                return 0;
-            }
-            bool fail = (m >= 1) && (del > RDIV * delp);
-            if (!fail) {
-                delp = del;
-                m++;
-                if (m >= NLS_MAXCOR) fail = true;
-            }
-            if (fail) {
-                if (!jc) { callSetup = true; jbad = true; acor = 0.0; m = 0; continue; }
-                break;
-            }
-        }
-        y = z[0] + acor;
-        return 1;
-    };
-
-    // ---- CVodeInit + first call ----
-    set_ewt();
-    z[1] = F(z[0]);
-    nfe++;
-    {   // cvHin
-        const double tout = tstop;
-        const double tdist = fabs(tout - tn);
-        const double tround = UROUND * fmax(fabs(tn), fabs(tout));
-        const double hlb = HLB_FACTOR * tround;
-        const double ratio = act ? fabs(z[1]) / (HUB_FACTOR * fabs(z[0]) + 1.0 / ewt) : 0.0;
-        const double hub_inv = uni(wave_max(ratio));
-        double hub = HUB_FACTOR * tdist;
-        if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
-        double hg = sqrt(hlb * hub);
-        if (hub < hlb) {
-            h = hg;
-        } else {
-            bool hnewOK = false;
-            double hnew = hg;
-            for (int count1 = 1; count1 <= MAX_ITERS; ++count1) {
-                y = hg * z[1] + z[0];
-                tempv = F(y);
-                nfe++;
-                tempv = (tempv - z[1]) * (1.0 / hg);
-                const double yddnrm = wrms(tempv);
-                if (hnewOK || count1 == MAX_ITERS) { hnew = hg; break; }
-                hnew = (yddnrm * hub * hub > 2.0) ? sqrt(2.0 / yddnrm) : sqrt(hg * hub);
-                const double hrat = hnew / hg;
-                if ((hrat > 0.5) && (hrat < 2.0)) hnewOK = true;
-                if ((count1 > 1) && (hrat > 2.0)) { hnew = hg; hnewOK = true; }
-                hg = hnew;
-            }
-            double h0 = H_BIAS * hnew;
-            if (h0 < hlb) h0 = hlb;
-            if (h0 > hub) h0 = hub;
-            h = h0;
-        }
-    }
-    if (o.hmax_inv > 0) { const double rh = fabs(h) * o.hmax_inv; if (rh > 1.0) h /= rh; }
-    if ((tn + h - tstop) * h > 0.0) h = (tstop - tn) * (1.0 - 4.0 * UROUND);
-    hscale = h; hprime = h;
-    if (trace) {
-        double* row = trace + (size_t)rid * (o.trace_cap + 1) * (n + 4);
-        if (lane == 0) { row[0] = 0.0; row[1] = h; row[2] = 1.0; row[3] = p_last; }
-        if (act) row[4 + lane] = z[0];
-    }
-    z[1] *= h;
-
-    int status = 0;
-    int nstloc = 0;
-    double u_out = z[0];
+    int perm = lane;
+    double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
     for (;;) {
-        if (nst > 0) set_ewt();
-        if (nstloc >= o.max_steps) { status = BR_ERR_MAXSTEPS; break; }
-        // ---- cvStep ----
-        const double saved_t = tn;
-        int ncf = 0, nef = 0, nflag = FIRST_CALL;
-        double dsm = 0.0;
-        int kflag = 0;
-        if ((nst > 0) && (hprime != h)) {
-            if (qprime != q) { adjust_order(qprime - q); q = qprime; L = q + 1; qwait = L; }
-            rescale();
+        const double y = V[V_Y * WAVE + lane];
+        double f;
+        {
+            const unsigned long long c0 = clock64();
+#ifndef BR_XNORHS
+            f = rhs(M, tb, S, T, Asv, Asv_th, y, lane, p_last);
+#else
+            f = y;
+#endif
+            cyc_rhs += clock64() - c0;
         }
-        for (;;) {
-            predict();
-            cvset();
-            const int r = nls(nflag);
-            if (r != 0) {
-                ncfn++;
-                restore(saved_t);
-                ncf++;
-                etamax = 1.0;
-                if ((fabs(h) <= hmin * ONEPSM) || (ncf == MXNCF)) { kflag = BR_ERR_CONV; break; }
-                eta = fmax(ETACF, hmin / fabs(h));
-                nflag = PREV_CONV_FAIL;
-                rescale();
-                continue;
+        double b = 0.0;
+        int act_code = ctl_post_rhs(C, V, lane, f, a, &b);
+        if (act_code == A_RHS) continue;
+        if (act_code == A_DONE) break;
+        int lu_fail = 0;
+        if (act_code == A_SETUP) {
+            if (ui(C->newj)) {
+                const unsigned long long c0 = clock64();
+#ifndef BR_XNOJAC
+                jacobian(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
+#endif
+                cyc_jac += clock64() - c0;
             }
-            dsm = acnrm * tq[2];
-            if (dsm <= 1.0) break;
-            nef++; netf++; nflag = PREV_ERR_FAIL;
-            restore(saved_t);
-            if ((fabs(h) <= hmin * ONEPSM) || (nef == MXNEF)) { kflag = BR_ERR_ERRTEST; break; }
-            etamax = 1.0;
-            if (nef <= MXNEF1) {
-                eta = 1.0 / (pow(BIAS2 * dsm, 1.0 / L) + ADDON);
-                eta = fmax(ETAMIN, fmax(eta, hmin / fabs(h)));
-                if (nef >= SMALL_NEF) eta = fmin(eta, ETAMXF);
-                rescale();
-                continue;
-            }
-            if (q > 1) {
-                eta = fmax(ETAMIN, hmin / fabs(h));
-                adjust_order(-1);
-                L = q; q--; qwait = L;
-                rescale();
-                continue;
-            }
-            eta = fmax(ETAMIN, hmin / fabs(h));
-            h *= eta; hscale = h; qwait = LONG_WAIT;
-            tempv = F(z[0]);
-            nfe++;
-            z[1] = h * tempv;
+            const unsigned long long c1 = clock64();
+            int pstep = 0;
+#ifndef BR_XNOLU
+            lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, pstep);
+#endif
+            perm = pivot_perm(pstep, lane, n);
+            cyc_lu += clock64() - c1;
         }
-        if (kflag) { status = kflag; break; }
-        // cvCompleteStep
-        nst++;
-#pragma unroll
-        for (int i = QMAX + 1; i >= 2; --i) if (i <= q) tau[i] = tau[i - 1];
-        if ((q == 1) && (nst > 1)) tau[2] = tau[1];
-        tau[1] = h;
-#pragma unroll
-        for (int j = 0; j <= QMAX; ++j) if (j <= q) z[j] += l[j] * acor;
-        qwait--;
-        if ((qwait == 1) && (q != QMAX)) { z[QMAX] = acor; saved_tq5 = tq[5]; }
-        // cvPrepareNextStep
-        if (etamax == 1.0) {
-            qwait = qwait > 2 ? qwait : 2;
-            qprime = q; hprime = h; eta = 1.0;
-        } else {
-            const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / L) + ADDON);
-            bool choose = (qwait == 0);
-            if (!choose) { eta = etaq; qprime = q; }
-            else {
-                qwait = 2;
-                double etaqm1 = 0.0, etaqp1 = 0.0;
-                if (q > 1) {
-                    double zq = 0.0;
-#pragma unroll
-                    for (int j = 0; j <= QMAX; ++j) if (j == q) zq = z[j];
-                    const double ddn = wrms(zq) * tq[1];
-                    etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / q) + ADDON);
-                }
-                if (q != QMAX && saved_tq5 != 0.0) {
-                    const double cquot = (tq[5] / saved_tq5) * pow(h / tau[2], (double)L);
-                    tempv = acor - cquot * z[QMAX];
-                    const double dup = wrms(tempv) * tq[3];
-                    etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (L + 1)) + ADDON);
-                }
-                const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
-                if (etam < THRESH) { eta = 1.0; qprime = q; }
-                else if (etam == etaq) { eta = etaq; qprime = q; }
-                else if (etam == etaqm1) { eta = etaqm1; qprime = q - 1; }
-                else { eta = etaqp1; qprime = q + 1; z[QMAX] = acor; }
-            }
-            // cvSetEta
-            if (eta < THRESH) { eta = 1.0; hprime = h; }
-            else {
-                eta = fmin(eta, etamax);
-                eta /= fmax(1.0, fabs(h) * o.hmax_inv * eta);
-                hprime = h * eta;
-            }
+        double delta = 0.0;
+        if (!lu_fail) {
+            const unsigned long long c0 = clock64();
+#ifndef BR_XNOSOLVE
+            delta = lu_solve<NMAX>(LUsave, n, lane, perm, b);
+#endif
+            cyc_sol += clock64() - c0;
         }
-        etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-        acor *= tq[2];
-        nstloc++;
-        if (o.ufac > 0.0) {   // runaway state (br_opts.unstable_factor)
-            const double mx = uni(wave_max(act ? fabs(z[0]) : 0.0));
-            if (!(mx <= ulimit)) { status = BR_ERR_UNSTABLE; break; }
-        }
-        if (trace && nst <= o.trace_cap) {   // per-step sample buffer (save_data rows)
-            double* row = trace + ((size_t)rid * (o.trace_cap + 1) + nst) * (n + 4);
-            if (lane == 0) { row[0] = tn; row[1] = h; row[2] = (double)q; row[3] = p_last; }
-            if (act) row[4 + lane] = z[0];
-        }
-        // CVode ONE_STEP + tstop handling
-        const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
-        if (fabs(tn - tstop) <= troundoff) {
-            // CVodeGetDky(tstop, 0)
-            const double s = (tstop - tn) / h;
-            double yv = 0.0;
-#pragma unroll
-            for (int j = QMAX; j >= 0; --j) {
-                if (j == q) yv = z[j];
-                else if (j < q) yv = z[j] + s * yv;
-            }
-            u_out = yv;
-            if (trace && nst <= o.trace_cap) {
-                double* row = trace + ((size_t)rid * (o.trace_cap + 1) + nst) * (n + 4);
-                if (lane == 0) row[0] = tstop;
-                if (act) row[4 + lane] = yv;
-            }
-            break;
-        }
-        if ((tn + hprime - tstop) * h > 0.0) {
-            hprime = (tstop - tn) * (1.0 - 4.0 * UROUND);
-            eta = hprime / h;
-        }
+        act_code = ctl_post_solve(C, V, lane, delta, lu_fail, a);
+        if (act_code == A_DONE) break;
     }
-    if (status) u_out = z[0];
+    const int status = ui(C->status);
+    const double u_out = status ? V[lane] : V[V_Y * WAVE + lane];
     if (act) U[(size_t)rid * n + lane] = u_out;
     if (stats && lane == 0) {
         double* st = stats + (size_t)rid * BR_NSTAT;
-        st[0] = (double)nst; st[1] = (double)nfe; st[2] = (double)nje; st[3] = (double)nsetups;
-        st[4] = (double)nni; st[5] = (double)ncfn; st[6] = (double)netf; st[7] = (double)status;
+        st[0] = (double)ui(C->nst); st[1] = (double)ui(C->nfe); st[2] = (double)ui(C->nje);
+        st[3] = (double)ui(C->nsetups); st[4] = (double)ui(C->nni); st[5] = (double)ui(C->ncfn);
+        st[6] = (double)ui(C->netf); st[7] = (double)status;
         st[8] = (double)(wall_clock64() - cyc0); st[9] = (double)cyc_rhs; st[10] = (double)cyc_jac;
-        st[11] = (double)cyc_lu; st[12] = (double)cyc_sol; st[13] = tn;
+        st[11] = (double)cyc_lu; st[12] = (double)cyc_sol; st[13] = ud(C->tn);
     }
 }
 
@@ -586,21 +691,19 @@ __global__ __launch_bounds__(256) void k_rates(DevMech M, int N, int rpb, const 
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
-    Smem S = carve(reinterpret_cast<double*>(W.rbase) + CTL_BYTES / 8, M);
+    const RView& S = W.R;
     const double T = Tv[rid], p = pv[rid];
     init_tconst(M, W.tb, S, T, lane);
     double c = 0.0;
     if (lane < M.ng) c = p * X[(size_t)rid * M.ng + lane] / (R_GAS * T);
     else if (lane < M.n) c = TH ? TH[(size_t)rid * M.ns + (lane - M.ng)] : 0.0;
-    if (lane < M.n) { S.conc[lane] = c; S.accw[lane] = 0.0; S.accs[lane] = 0.0; }
+    if (lane < M.n) { S.sp[lane] = c; S.sp[64 + lane] = 0.0; S.sp[128 + lane] = 0.0; }
     const double Ctot = wave_sum(lane < M.ng ? c : 0.0);
     wave_sync();
-    third_body(M, W.tb, S, Ctot, lane);
+    production(M, W.tb, S, R_GAS * T, Ctot, lane);
     wave_sync();
-    production(M, W.tb, S, R_GAS * T, lane);
-    wave_sync();
-    const double w = lane < M.n ? S.accw[lane] : 0.0;
-    const double s = lane < M.n ? S.accs[lane] : 0.0;
+    const double w = lane < M.n ? S.sp[64 + lane] : 0.0;
+    const double s = lane < M.n ? S.sp[128 + lane] : 0.0;
     if (lane < M.ng) W_[(size_t)rid * M.ng + lane] = w;
     if (SD && lane < M.n) SD[(size_t)rid * M.n + lane] = s;
 }
@@ -612,15 +715,14 @@ __global__ __launch_bounds__(256) void k_rhs(DevMech M, int N, int rpb, const do
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
-    Smem S = carve(reinterpret_cast<double*>(W.rbase) + CTL_BYTES / 8, M);
+    const RView& S = W.R;
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
     init_tconst(M, W.tb, S, T, lane);
     const bool act = lane < M.n;
     const double u = act ? U[(size_t)rid * M.n + lane] : 0.0;
-    const double Mk = act ? M.molwt[lane] : 1.0;
-    const double du = rhs(M, W.tb, S, T, Asv, Asv_th, u, lane, Mk, reinterpret_cast<double*>(W.rbase) + 8);
+    const double du = rhs(M, W.tb, S, T, Asv, Asv_th, u, lane, reinterpret_cast<double*>(W.rbase));
     if (act) DU[(size_t)rid * M.n + lane] = du;
 }
 
@@ -632,16 +734,15 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
-    Smem S = carve(reinterpret_cast<double*>(W.rbase) + CTL_BYTES / 8, M);
+    const RView& S = W.R;
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
     init_tconst(M, W.tb, S, T, lane);
     const bool act = lane < M.n;
     const double u = act ? U[(size_t)rid * M.n + lane] : 0.0;
-    const double Mk = act ? M.molwt[lane] : 1.0;
-    double* Jsave = Jws + (size_t)rid * NMAX * WAVE;
-    jacobian(M, W.tb, S, T, Asv, Asv_th, u, lane, Mk, Jsave);
+    double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);
+    jacobian(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + 2 * NMAX * WAVE);
     if (act) {
         double* row = J + ((size_t)rid * M.n + lane) * M.n;
 #pragma unroll
@@ -714,31 +815,19 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     const int ng = d->ng, ns = d->ns, nrg = d->nrg, nrs = d->nrs, n = ng + ns;
     if (ng <= 0 || ns < 0 || nrg < 0 || nrs < 0) return fail(BR_ERR_INPUT, "bad sizes");
     if (n > 64) return fail(BR_ERR_UNSUPPORTED, "n > 64 components is not supported by this build");
-    if (nrg + nrs > 65535) return fail(BR_ERR_UNSUPPORTED, "too many reactions");
     HIPCHK(hipSetDevice(device));
     br_mech* m = new br_mech();
     m->device = device; m->ng = ng; m->ns = ns; m->nrg = nrg; m->nrs = nrs; m->n = n;
     m->nmax = n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : 64));
     DevMech& M = m->dm;
-    M.ng = ng; M.ns = ns; M.n = n; M.nrg = nrg; M.nrs = nrs; M.nr = nrg + nrs; M.conv = d->conv;
+    M.ng = ng; M.ns = ns; M.n = n; M.nrg = nrg; M.nrs = nrs; M.conv = d->conv;
     M.p_std = d->p_std > 0 ? d->p_std : 1e5;
     M.G = d->site_density * 1e4;
-    std::vector<double> molwt(n, 1.0), sigma(n, 1.0), nasa((size_t)ng * 15);
-    for (int k = 0; k < ng; ++k) molwt[k] = d->molwt[k];
-    for (int i = 0; i < ns; ++i) sigma[ng + i] = d->sigma ? d->sigma[i] : 1.0;
-    for (size_t i = 0; i < (size_t)ng * 15; ++i) nasa[i] = d->nasa[i];
     auto pack4 = [](const int* v, int cnt) {
         uint32_t w = 0;
         for (int e = 0; e < 4; ++e) w |= (uint32_t)(e < cnt ? (v[e] & 255) : 255) << (8 * e);
         return w;
     };
-    // ---- gas reactions, evaluated in a permuted order (falloff, then +M, then elementary) so
-    //      that the lanes of one pass take the same branch; results are per species, so the
-    //      order is invisible outside the kernel
-    std::vector<int> perm;
-    for (int pass = 2; pass >= 0; --pass)
-        for (int r = 0; r < nrg; ++r) if (d->g_tb[r] == pass) perm.push_back(r);
-    std::vector<uint32_t> rx_sp(nrg), rx_pr(nrg), rx_info(nrg), rx_sc(3 * (size_t)nrg);
     // net-stoichiometry scatter list of a reaction: up to 6 (species, nu != 0) pairs packed in
     // 3 words: w0 = species 0..3, w1 = species 4..5 | count << 16, w2 = 4-bit signed nu x 6
     auto scatter_pack = [](const int* f, int nf, const int* pr, int np, uint32_t* w) -> bool {
@@ -749,134 +838,161 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         };
         for (int e = 0; e < nf; ++e) add(f[e], -1);
         for (int e = 0; e < np; ++e) add(pr[e], 1);
-        int m = 0;
+        int mm = 0;
         w[0] = w[1] = w[2] = 0;
         for (int i = 0; i < c; ++i) {
             if (nu[i] == 0) continue;
-            if (m >= 6 || nu[i] < -8 || nu[i] > 7) return false;
-            if (m < 4) w[0] |= (uint32_t)(sp[i] & 255) << (8 * m);
-            else w[1] |= (uint32_t)(sp[i] & 255) << (8 * (m - 4));
-            w[2] |= (uint32_t)(nu[i] & 15) << (4 * m);
-            ++m;
+            if (mm >= 6 || nu[i] < -8 || nu[i] > 7) return false;
+            if (mm < 4) w[0] |= (uint32_t)(sp[i] & 255) << (8 * mm);
+            else w[1] |= (uint32_t)(sp[i] & 255) << (8 * (mm - 4));
+            w[2] |= (uint32_t)(nu[i] & 15) << (4 * mm);
+            ++mm;
         }
-        w[1] |= (uint32_t)m << 16;
+        w[1] |= (uint32_t)mm << 16;
         return true;
     };
-    std::vector<int> gdnu(nrg);
-    std::vector<double> garr(3 * (size_t)std::max(nrg, 1), 0.0), gkcs(std::max(nrg, 1), 1.0);
+    // ---- gas reactions, evaluated in a permuted order (falloff, then +M, then elementary) so
+    //      that the lanes of one pass take the same branch; results are per species, so the
+    //      order is invisible outside the kernel
+    std::vector<int> perm;
+    for (int pass = 2; pass >= 0; --pass)
+        for (int r = 0; r < nrg; ++r) if (d->g_tb[r] == pass) perm.push_back(r);
     int ntb = 0, nfo = 0;
-    std::vector<int> fo_of(nrg, -1), tb_of(nrg, -1);
     for (int i = 0; i < nrg; ++i) {
-        const int r = perm[i];
-        if (d->g_tb[r] == 2) fo_of[r] = nfo++;
-        if (d->g_tb[r]) tb_of[r] = ntb++;
+        if (d->g_tb[perm[i]] == 2) nfo++;
+        if (d->g_tb[perm[i]]) ntb++;
     }
     if (ntb > 1023 || nfo > 1023) { delete m; return fail(BR_ERR_UNSUPPORTED, "too many third-body reactions"); }
-    std::vector<double> folow(3 * (size_t)std::max(nfo, 1), 0.0), fotroe(4 * (size_t)std::max(nfo, 1), 0.0);
-    std::vector<int> fontroe(std::max(nfo, 1), 0);
-    std::vector<int> tbptr(1, 0);
-    std::vector<uint32_t> tbsp;
-    std::vector<double> tbde, tbeff;
+    std::vector<uint32_t> rx(RX_WORDS * (size_t)nrg, 0);
+    std::vector<double> gpar(4 * (size_t)std::max(nrg, 1), 0.0), fopar(8 * (size_t)std::max(nfo, 1), 0.0);
+    std::vector<int> gdnu(std::max(nrg, 1), 0);
+    std::vector<std::pair<int, double>> tbe;       // (species, eff - 1)
+    std::vector<double> tbeff;                     // dense [ntb][n]
+    int tbi = 0, foi = 0;
     for (int i = 0; i < nrg; ++i) {
         const int r = perm[i];
         const int nf = d->g_nf[r], nr = d->g_nr[r], tb = d->g_tb[r];
         if (nf > 4 || nr > 4 || nf < 1) { delete m; return fail(BR_ERR_UNSUPPORTED, "reaction with >4 entries"); }
-        rx_sp[i] = pack4(d->g_f + r * 4, nf);
-        rx_pr[i] = pack4(d->g_r + r * 4, nr);
-        if (!scatter_pack(d->g_f + r * 4, nf, d->g_r + r * 4, nr, &rx_sc[3 * (size_t)i])) {
+        uint32_t* rec = &rx[RX_WORDS * (size_t)i];
+        rec[0] = pack4(d->g_f + r * 4, nf);
+        rec[1] = pack4(d->g_r + r * 4, nr);
+        if (!scatter_pack(d->g_f + r * 4, nf, d->g_r + r * 4, nr, rec + 4)) {
             delete m; return fail(BR_ERR_UNSUPPORTED, "reaction touches more than 6 species");
         }
-        for (int c = 0; c < 3; ++c) garr[(size_t)c * nrg + i] = d->g_arr[r * 3 + c];
+        for (int c = 0; c < 3; ++c) gpar[4 * (size_t)i + c] = d->g_arr[r * 3 + c];
+        gpar[4 * (size_t)i + 3] = ((d->conv & BR_CONV_KC_UNIT_SLIP) && tb != 2) ? std::pow(1e6, (double)(nr - nf)) : 1.0;
         gdnu[i] = nr - nf;
-        if ((d->conv & BR_CONV_KC_UNIT_SLIP) && tb != 2) gkcs[i] = std::pow(1e6, (double)(nr - nf));
-        int tbidx = 0, foidx = 0;
+        int troe = 0, fo = 0, tbidx = 0;
         if (tb) {
-            tbidx = tb_of[r];
+            tbidx = tbi++;
+            const int start = (int)tbe.size();
             for (int k = 0; k < ng; ++k) {
                 const double e = d->g_eff[(size_t)r * ng + k];
-                if (e != 1.0) { tbsp.push_back((uint32_t)k); tbde.push_back(e - 1.0); }
+                if (e != 1.0) tbe.push_back({k, e - 1.0});
             }
-            tbptr.push_back((int)tbsp.size());
+            const int cnt = (int)tbe.size() - start;
+            if (start >= (1 << 20) || cnt >= (1 << 12)) { delete m; return fail(BR_ERR_UNSUPPORTED, "third-body list too long"); }
+            rec[3] = (uint32_t)start | ((uint32_t)cnt << 20);
             for (int k = 0; k < n; ++k) tbeff.push_back(k < ng ? d->g_eff[(size_t)r * ng + k] : 0.0);
         }
         if (tb == 2) {
-            foidx = fo_of[r];
-            for (int c = 0; c < 3; ++c) folow[(size_t)c * nfo + foidx] = d->g_low[r * 3 + c];
-            fontroe[foidx] = d->g_troe_n[r];
-            for (int c = 0; c < 4; ++c) fotroe[(size_t)c * nfo + foidx] = d->g_troe[r * 4 + c];
+            fo = foi++;
+            troe = d->g_troe_n[r];
+            for (int c = 0; c < 3; ++c) fopar[8 * (size_t)fo + c] = d->g_low[r * 3 + c];
+            for (int c = 0; c < 4; ++c) fopar[8 * (size_t)fo + 3 + c] = d->g_troe[r * 4 + c];
+            fopar[8 * (size_t)fo + 7] = troe;
         }
-        rx_info[i] = (uint32_t)(nf | (nr << 3) | ((d->g_rev[r] ? 1 : 0) << 6) | (tb << 7) | (tbidx << 9) | (foidx << 19));
+        rec[2] = (uint32_t)(nf | (nr << 3) | ((d->g_rev[r] ? 1 : 0) << 6) | (tb << 7) | ((troe & 7) << 9) |
+                            (fo << 12) | (tbidx << 22));
     }
-    M.ntb = ntb; M.nfo = nfo; M.ntbe = (int)tbsp.size();
+    M.ntb = ntb; M.nfo = nfo; M.ntbe = (int)tbe.size();
     // ---- surface reactions
-    std::vector<uint32_t> sx_sp(2 * (size_t)nrs), sx_pr(2 * (size_t)nrs), sx_info(nrs), scs(std::max(nrs, 1), 0);
-    std::vector<uint32_t> sx_sc(3 * (size_t)nrs);
-    std::vector<double> sarr(3 * (size_t)std::max(nrs, 1), 0.0), sce(4 * (size_t)std::max(nrs, 1), 0.0);
+    std::vector<uint32_t> sx(SX_WORDS * (size_t)nrs, 0);
+    std::vector<double> sxe(4 * (size_t)nrs, 0.0), spar(4 * (size_t)std::max(nrs, 1), 0.0);
     for (int r = 0; r < nrs; ++r) {
         const int nf = d->s_nf[r], np = d->s_np[r], nc = d->s_ncov[r];
         if (nf > 6 || np > 6 || nc > 4) { delete m; return fail(BR_ERR_UNSUPPORTED, "surface reaction too large"); }
+        uint32_t* rec = &sx[SX_WORDS * (size_t)r];
         int e6[6];
         for (int e = 0; e < 6; ++e) e6[e] = e < nf ? d->s_f[r * 6 + e] : 255;
-        sx_sp[2 * r] = pack4(e6, 4);
-        sx_sp[2 * r + 1] = pack4(e6 + 4, 2);
+        rec[0] = pack4(e6, 4);
+        rec[1] = pack4(e6 + 4, 2);
         int p6[6];
         for (int e = 0; e < 6; ++e) p6[e] = e < np ? d->s_p[r * 6 + e] : 255;
-        sx_pr[2 * r] = pack4(p6, 4);
-        sx_pr[2 * r + 1] = pack4(p6 + 4, 2);
-        if (!scatter_pack(d->s_f + r * 6, nf, d->s_p + r * 6, np, &sx_sc[3 * (size_t)r])) {
+        rec[2] = pack4(p6, 4);
+        rec[3] = pack4(p6 + 4, 2);
+        if (!scatter_pack(d->s_f + r * 6, nf, d->s_p + r * 6, np, rec + 6)) {
             delete m; return fail(BR_ERR_UNSUPPORTED, "surface reaction touches more than 6 species");
         }
-        for (int c = 0; c < 3; ++c) sarr[(size_t)c * nrs + r] = d->s_arr[r * 3 + c];
         int cs[4] = {0, 0, 0, 0};
-        for (int c = 0; c < nc; ++c) { cs[c] = d->s_cov_sp[r * 4 + c]; sce[(size_t)c * nrs + r] = d->s_cov_eps[r * 4 + c]; }
-        scs[r] = pack4(cs, 4);
+        for (int c = 0; c < nc; ++c) { cs[c] = d->s_cov_sp[r * 4 + c]; sxe[4 * (size_t)r + c] = d->s_cov_eps[r * 4 + c]; }
+        rec[5] = pack4(cs, 4);
         int g = -1;
         for (int e = 0; e < nf; ++e) if (d->s_f[r * 6 + e] < ng) g = d->s_f[r * 6 + e];
         if (d->s_stick[r] && g < 0) { delete m; return fail(BR_ERR_INPUT, "sticking reaction without gas reactant"); }
-        sx_info[r] = (uint32_t)(nf | (np << 3) | ((d->s_stick[r] ? 1 : 0) << 6) | (nc << 7) | ((g < 0 ? 0 : g) << 10));
+        rec[4] = (uint32_t)(nf | (np << 3) | ((d->s_stick[r] ? 1 : 0) << 6) | (nc << 7) | ((g < 0 ? 0 : g) << 10));
+        for (int c = 0; c < 3; ++c) spar[4 * (size_t)r + c] = d->s_arr[r * 3 + c];
+        spar[4 * (size_t)r + 3] = g >= 0 ? d->molwt[g] : 1.0;
     }
     // ---- Jacobian column lists: reactions whose rate depends on component j
     std::vector<int> colptr(1, 0), colrx;
     for (int j = 0; j < n; ++j) {
-        std::vector<int> rs;
         for (int i = 0; i < nrg; ++i) {
             const int r = perm[i];
             bool dep = false;
             for (int e = 0; e < d->g_nf[r]; ++e) dep |= d->g_f[r * 4 + e] == j;
             for (int e = 0; e < d->g_nr[r]; ++e) dep |= d->g_r[r * 4 + e] == j;
             if (d->g_tb[r] && j < ng && d->g_eff[(size_t)r * ng + j] != 0.0) dep = true;
-            if (dep) rs.push_back(i);
+            if (dep) colrx.push_back(i);
         }
         for (int r = 0; r < nrs; ++r) {
             bool dep = false;
             for (int e = 0; e < d->s_nf[r]; ++e) dep |= d->s_f[r * 6 + e] == j;
             for (int c = 0; c < d->s_ncov[r]; ++c) dep |= d->s_cov_sp[r * 4 + c] == j;
-            if (dep) rs.push_back(nrg + r);
+            if (dep) colrx.push_back(nrg + r);
         }
-        for (int r : rs) colrx.push_back(r);
         colptr.push_back((int)colrx.size());
     }
-    // ---- packed LDS table image
-    M.tab_words = tab_words(nrg, nrs, ntb, M.ntbe);
-    std::vector<uint32_t> tab(M.tab_words, 0);
+    // ---- LDS table image: molwt[64] | sigma[64] | RX | SX | SXE | TBE
+    auto al16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t off = IMG_RX_OFF + al16(RX_WORDS * 4 * (size_t)nrg);
+    M.sx_off = (int)off;
+    off += al16(SX_WORDS * 4 * (size_t)nrs);
+    M.sxe_off = (int)off;
+    off += al16(32 * (size_t)nrs);
+    M.tbe_off = (int)off;
+    off += al16(16 * tbe.size());
+    M.img_bytes = (int)al16(off);
+    std::vector<unsigned char> img(M.img_bytes, 0);
     {
-        size_t o = 0;
-        auto put = [&](const std::vector<uint32_t>& v) { for (uint32_t x : v) tab[o++] = x; };
-        put(rx_sp); put(rx_pr); put(rx_info); put(rx_sc); put(sx_sp); put(sx_pr); put(sx_info); put(sx_sc);
-        std::vector<uint32_t> tp(tbptr.begin(), tbptr.end());
-        put(tp); put(tbsp);
+        double* mw = reinterpret_cast<double*>(img.data());
+        for (int k = 0; k < 64; ++k) { mw[k] = 1.0; mw[64 + k] = 1.0; }
+        for (int k = 0; k < ng; ++k) mw[k] = d->molwt[k];
+        for (int i = 0; i < ns; ++i) mw[64 + ng + i] = d->sigma ? d->sigma[i] : 1.0;
+        if (nrg) memcpy(img.data() + IMG_RX_OFF, rx.data(), rx.size() * 4);
+        if (nrs) memcpy(img.data() + M.sx_off, sx.data(), sx.size() * 4);
+        if (nrs) memcpy(img.data() + M.sxe_off, sxe.data(), sxe.size() * 8);
+        for (size_t i = 0; i < tbe.size(); ++i) {
+            unsigned char* e = img.data() + M.tbe_off + 16 * i;
+            const int sp = tbe[i].first;
+            memcpy(e, &sp, 4);
+            memcpy(e + 8, &tbe[i].second, 8);
+        }
     }
+    M.fod_off = fod_off_bytes(nrg);
+    M.skd_off = skd_off_bytes(nrg, nfo);
+    M.rblock_bytes = rblock_bytes(nrg, nfo, nrs);
+    std::vector<double> nasa((size_t)ng * 15);
+    for (size_t i = 0; i < (size_t)ng * 15; ++i) nasa[i] = d->nasa[i];
     if (tbeff.empty()) tbeff.push_back(0.0);
-    if (tbde.empty()) tbde.push_back(0.0);
     if (colrx.empty()) colrx.push_back(0);
+    std::vector<uint4> imgv(M.img_bytes / 16);
+    memcpy(imgv.data(), img.data(), M.img_bytes);
     int rc = 0;
-    rc |= upload(m, tab, &M.tab); rc |= upload(m, tbde, &M.tab_d);
-    rc |= upload(m, molwt, &M.molwt); rc |= upload(m, sigma, &M.sigma); rc |= upload(m, nasa, &M.nasa);
-    rc |= upload(m, garr, &M.g_arr); rc |= upload(m, gkcs, &M.g_kcs); rc |= upload(m, gdnu, &M.g_dnu);
-    rc |= upload(m, folow, &M.fo_low); rc |= upload(m, fotroe, &M.fo_troe); rc |= upload(m, fontroe, &M.fo_ntroe);
-    rc |= upload(m, tbeff, &M.tb_eff);
-    rc |= upload(m, sarr, &M.s_arr); rc |= upload(m, scs, &M.s_cov_sp); rc |= upload(m, sce, &M.s_cov_eps);
-    rc |= upload(m, colptr, &M.col_ptr); rc |= upload(m, colrx, &M.col_rx);
+    rc |= upload(m, imgv, &M.img);
+    rc |= upload(m, nasa, &M.nasa); rc |= upload(m, gpar, &M.g_par); rc |= upload(m, gdnu, &M.g_dnu);
+    rc |= upload(m, fopar, &M.fo_par); rc |= upload(m, spar, &M.s_par);
+    rc |= upload(m, tbeff, &M.tb_eff); rc |= upload(m, colptr, &M.col_ptr); rc |= upload(m, colrx, &M.col_rx);
     if (rc) { br_mech_destroy(m); return rc; }
     // ---- reactors (waves) per workgroup: the value that maximises resident waves per CU,
     //      from the occupancy calculator (VGPRs, LDS: tables once per workgroup + one block
@@ -925,7 +1041,7 @@ static int ensure_ws(br_mech* m, size_t bytes) {
     return 0;
 }
 static int ensure_jws(br_mech* m, int N) {
-    const size_t bytes = (size_t)N * std::max(2 * m->nmax, 64) * WAVE * sizeof(double);
+    const size_t bytes = (size_t)N * ws_doubles(std::max(m->nmax, 64), m->nrg) * sizeof(double);
     if (m->jws_bytes >= bytes) return 0;
     if (m->jws) hipFree(m->jws);
     m->jws = nullptr; m->jws_bytes = 0;
@@ -1116,9 +1232,14 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     double* Jt = ws + (size_t)rid * 2 * NMAX * WAVE;
     double* LU = Jt + NMAX * WAVE;
     for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
-    __shared__ int ps[64];
-    const int f = lu_factor_mem<NMAX>(Jt, LU, g[rid], n, lane, &ps[lane]);
-    const double r = lu_solve_mem<NMAX>(LU, n, lane, ps[lane], lane < n ? b[(size_t)rid * n + lane] : 0.0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    int pstep = 0;
+    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, pstep);
+    const int perm = pivot_perm(pstep, lane, n);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0);
     if (lane < n) x[(size_t)rid * n + lane] = r;
     if (lane == 0) fail[rid] = f;
 }

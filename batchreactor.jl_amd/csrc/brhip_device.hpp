@@ -2,19 +2,19 @@
 //
 // Execution model: ONE REACTOR PER WAVEFRONT (64 lanes), several reactors (waves) per
 // workgroup; lane k <-> solution component k (gas species 0..ng-1, then surface coverages).
-//  * The compact mechanism tables (reaction species packs, production CSR, third-body
-//    efficiencies) are staged ONCE PER WORKGROUP into LDS and shared by its waves.
-//  * T-dependent rate constants live in a per-reactor LDS block (T is a per-reactor
-//    constant: ConstantParams, src/BatchReactor.jl:14-17), as does the BDF controller state.
-//  * Reactions are evaluated lane-parallel (reaction r on lane r mod 64) and accumulated
-//    into the species production sums with fp64 LDS atomics (ds_add_f64, wave-private).
-//  * Reductions are DPP row reductions + 4 v_readlane (no LDS round trips).
-//  * The Newton matrix I - gamma*J is factored ROW-PER-LANE in registers (a[NMAX]); the
-//    pivot row of each LU step is found by a DPP argmax and broadcast with v_readlane; no row
-//    swaps; the pivot order is recovered with a ballot. J and the LU factors are kept in a
-//    per-reactor HBM workspace (coalesced [column][lane]) so the step loop's register file
-//    stays small.
-// Waves of one workgroup never synchronise with each other after the table staging.
+//
+// LDS layout (few base addresses, so the hot loop keeps few SGPRs live):
+//  * table image, staged once per workgroup from global memory (host-built, `img`):
+//      [0,512) molwt[64] | [512,1024) sigma[64] | RX records (32 B / gas reaction) |
+//      SX records (48 B / surface reaction) | SXE (4 doubles / surface reaction: coverage eps) |
+//      TBE third-body entries (16 B: species, eff-1)
+//  * per reactor block: [Ctl][V: Nordsieck + work vectors][SP: conc | accw | accs (64 each)]
+//      [RXD: {kf, kr} per gas reaction][FOD: {k0, log10 Fcent, c, n} per falloff reaction]
+//      [SKD: {k, k*exp(cov)} per surface reaction]
+//  * T-dependent rate constants (RXD/FOD/SKD) are computed once per reactor: T is a per-reactor
+//    constant (ConstantParams, src/BatchReactor.jl:14-17).
+// Reactions are evaluated lane-parallel (reaction r on lane r mod 64); production rates are
+// accumulated with fp64 LDS atomics (ds_add_f64, no return); reductions are DPP + readlane.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,77 +25,65 @@ constexpr double R_GAS = 8.31446261815324;   // RxnHelperUtils.R (src/BatchReact
 constexpr int WAVE = 64;
 
 // ------------------------------------------------------------------------------------
-// mechanism description (global memory pointers) and the LDS table layout
+// mechanism description (host-built)
 // ------------------------------------------------------------------------------------
 struct DevMech {
-    int ng, ns, n, nrg, nrs, nr, conv;
-    int ntb, nfo, ntbe;
+    int ng, ns, n, nrg, nrs, ntb, nfo, ntbe, conv;
     double p_std, G;              // Pa ; site density mol/m2
-    // words staged to LDS (uint32): [rx_sp nrg][rx_pr nrg][rx_info nrg][sx_sp 2*nrs][sx_pr 2*nrs]
-    // [sx_info nrs][tb_ptr ntb+1][tb_sp ntbe]  then doubles [tb_de ntbe]
-    const uint32_t* tab;          // packed words
-    int tab_words;                // number of uint32 words (16-byte multiple)
-    const double* tab_d;          // tb_de
-    // global-only (init / Jacobian)
-    const double* molwt;          // [n] (1 for surface)
-    const double* sigma;          // [n] (1 for gas)
-    const double* nasa;           // [ng*15]
-    const double* g_arr;          // [3][nrg]
-    const double* g_kcs;          // [nrg]
+    const uint4* img;             // LDS table image (global copy)
+    int img_bytes;                // multiple of 16
+    int sx_off, sxe_off, tbe_off; // byte offsets in the image
+    int fod_off, skd_off;         // byte offsets of FOD / SKD from the reactor's RXD base
+    int rblock_bytes;             // per-reactor LDS bytes from SP start (SP + RXD + FOD + SKD)
+    // init only (T-dependent constants)
+    const double* nasa;           // [ng][15]: Tmid, a_hi[7], a_lo[7]
+    const double* g_par;          // [nrg][4]: A (SI), beta, Ea/R, Kc scale
     const int* g_dnu;             // [nrg]
-    const double* fo_low;         // [3][nfo]
-    const double* fo_troe;        // [4][nfo]
-    const int* fo_ntroe;          // [nfo]
-    const double* tb_eff;         // [ntb][n] dense (Jacobian)
-    const double* s_arr;          // [3][nrs]
-    const uint32_t* s_cov_sp;     // [nrs] 4 x 8-bit species
-    const double* s_cov_eps;      // [4][nrs]
+    const double* fo_par;         // [nfo][8]: A0, b0, E0/R, a, T***, T*, T**, ntroe
+    const double* s_par;          // [nrs][4]: A or s0, beta, Ea [J/mol], M_gas (stick)
+    // Jacobian only
+    const double* tb_eff;         // [ntb][n] dense efficiencies
     const int* col_ptr;           // [n+1] Jacobian column lists
     const int* col_rx;            // combined reaction index (gas r, surface nrg+r)
 };
 
-// rx_info bit fields
+// RX record: w0 reactant species (4 x 8 bit, 255 pad), w1 product species, w2 info,
+// w3 third-body list (start | count << 20), w4..w6 net-stoichiometry scatter list, w7 pad
 __host__ __device__ inline int gi_nf(uint32_t v) { return v & 7; }
 __host__ __device__ inline int gi_nr(uint32_t v) { return (v >> 3) & 7; }
 __host__ __device__ inline int gi_rev(uint32_t v) { return (v >> 6) & 1; }
 __host__ __device__ inline int gi_tb(uint32_t v) { return (v >> 7) & 3; }
-__host__ __device__ inline int gi_tbidx(uint32_t v) { return (v >> 9) & 1023; }
-__host__ __device__ inline int gi_foidx(uint32_t v) { return (v >> 19) & 1023; }
-// sx_info bit fields
+__host__ __device__ inline int gi_troe(uint32_t v) { return (v >> 9) & 7; }
+__host__ __device__ inline int gi_foidx(uint32_t v) { return (v >> 12) & 1023; }
+__host__ __device__ inline int gi_tbidx(uint32_t v) { return (v >> 22) & 1023; }
+// SX record: w0,w1 reactants (6 x 8 bit), w2,w3 products, w4 info, w5 coverage species (4 x 8),
+// w6..w8 scatter list, w9..w11 pad
 __host__ __device__ inline int si_nf(uint32_t v) { return v & 7; }
 __host__ __device__ inline int si_np(uint32_t v) { return (v >> 3) & 7; }
 __host__ __device__ inline int si_stick(uint32_t v) { return (v >> 6) & 1; }
 __host__ __device__ inline int si_ncov(uint32_t v) { return (v >> 7) & 7; }
 __host__ __device__ inline int si_gas(uint32_t v) { return (v >> 10) & 255; }
 __host__ __device__ inline int sp8(uint32_t w, int e) { return (w >> (8 * e)) & 255; }
+constexpr int RX_WORDS = 8, SX_WORDS = 12;
+constexpr int IMG_RX_OFF = 1024;
 
-struct Tab {   // LDS views
-    const uint32_t *rx_sp, *rx_pr, *rx_info, *rx_sc, *sx_sp, *sx_pr, *sx_info, *sx_sc, *tb_ptr, *tb_sp;
-    const double* tb_de;
+struct Tab {   // views of the staged table image
+    const double* molwt;   // [64]
+    const double* sigma;   // [64]
+    const uint32_t* rx;    // RX_WORDS per gas reaction
+    const uint32_t* sx;    // SX_WORDS per surface reaction
+    const double* sxe;     // 4 per surface reaction
+    const char* tbe;       // 16 B per third-body entry
 };
-
-__host__ __device__ inline int tab_words(int nrg, int nrs, int ntb, int ntbe) {
-    int w = 6 * nrg + 8 * nrs + (ntb + 1) + ntbe;
-    return (w + 3) & ~3;   // 16-byte multiple
-}
-__device__ __forceinline__ Tab tab_view(const uint32_t* base, const DevMech& M) {
+__device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
     Tab t;
-    const uint32_t* p = base;
-    t.rx_sp = p; p += M.nrg;
-    t.rx_pr = p; p += M.nrg;
-    t.rx_info = p; p += M.nrg;
-    t.rx_sc = p; p += 3 * M.nrg;
-    t.sx_sp = p; p += 2 * M.nrs;
-    t.sx_pr = p; p += 2 * M.nrs;
-    t.sx_info = p; p += M.nrs;
-    t.sx_sc = p; p += 3 * M.nrs;
-    t.tb_ptr = p; p += M.ntb + 1;
-    t.tb_sp = p;
-    t.tb_de = reinterpret_cast<const double*>(base + M.tab_words);
+    t.molwt = reinterpret_cast<const double*>(base);
+    t.sigma = t.molwt + 64;
+    t.rx = reinterpret_cast<const uint32_t*>(base + IMG_RX_OFF);
+    t.sx = reinterpret_cast<const uint32_t*>(base + M.sx_off);
+    t.sxe = reinterpret_cast<const double*>(base + M.sxe_off);
+    t.tbe = base + M.tbe_off;
     return t;
-}
-__host__ __device__ inline size_t tab_bytes(const DevMech& M) {
-    return ((size_t)M.tab_words * 4 + (size_t)M.ntbe * 8 + 15) & ~(size_t)15;
 }
 
 // ------------------------------------------------------------------------------------
@@ -112,10 +100,6 @@ __device__ __forceinline__ double dppd(double v) {
     const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-template <int CTRL>
-__device__ __forceinline__ int dppi(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
 __device__ __forceinline__ double bcast(double v, int lane) {
     const long long b = __double_as_longlong(v);
@@ -147,81 +131,52 @@ __device__ __forceinline__ double wave_max(double v) {
     v = fmax(v, dppd<0x140>(v));
     return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
 }
-template <int CTRL>
-__device__ __forceinline__ void argmax_step(double& v, int& i) {
-    const double ov = dppd<CTRL>(v);
-    const int oi = dppi<CTRL>(i);
-    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+
+// opaque copy of a uniform pointer: addresses derived from it cannot be hoisted out of the
+// integrator's main loop (otherwise LICM keeps ~NMAX 64-bit column addresses live across the
+// whole loop and the kernel spills)
+template <class T>
+__device__ __forceinline__ T* launder(T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
 }
-// lane of the largest v (lowest lane on ties); uniform
-__device__ __forceinline__ int wave_argmax(double v) {
-    int i = (int)threadIdx.x & 63;
-    argmax_step<0xB1>(v, i);
-    argmax_step<0x4E>(v, i);
-    argmax_step<0x141>(v, i);
-    argmax_step<0x140>(v, i);
-    double bv = bcast(v, 0);
-    int bi = __builtin_amdgcn_readlane(i, 0);
-#pragma unroll
-    for (int r = 16; r < 64; r += 16) {
-        const double rv = bcast(v, r);
-        const int ri = __builtin_amdgcn_readlane(i, r);
-        if (rv > bv || (rv == bv && ri < bi)) { bv = rv; bi = ri; }
-    }
-    return uni(bi);
+// opaque copy of a per-lane value (stops LICM from hoisting lane-dependent constants such as
+// the identity-matrix entries of I - gamma*J out of the main loop)
+__device__ __forceinline__ int launder_v(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 // ------------------------------------------------------------------------------------
-// per-reactor LDS workspace
+// per-reactor rate workspace (LDS)
 // ------------------------------------------------------------------------------------
-struct Smem {
-    double* kf;    // [nrg]
-    double* kr;    // [nrg]
-    double* jpre;  // [nrg]  Jacobian: multiplier of dD
-    double* jdm;   // [nrg]  Jacobian: D * d(pre)/d[M]
-    double* accw;  // [max(n, ng)] production by gas reactions (also g/RT scratch at init)
-    double* accs;  // [n]    production by surface reactions
-    double* ks;    // [nrs]
-    double* sk;    // [nrs]
-    double* k0;    // [nfo]
-    double* lfc;   // [nfo]  log10(Fcent)
-    double* tcc;   // [nfo]  Troe c
-    double* tnn;   // [nfo]  Troe n
-    double* conc;  // [n]    gas concentrations (mol/m3) then coverages
-    double* mc;    // [ntb]
+struct RView {
+    double* sp;    // conc[k] = sp[k], accw[k] = sp[64+k], accs[k] = sp[128+k]
+    double* rxd;   // kf = rxd[2r], kr = rxd[2r+1]
+    double* fod;   // k0, log10 Fcent, c, n per falloff reaction
+    double* skd;   // k(T), k*exp(-sum eps theta/RT) (Jacobian) per surface reaction
 };
-
-__host__ __device__ inline int accw_len(int n, int ng) { return n > ng ? n : ng; }
-__host__ __device__ inline size_t reactor_doubles(const DevMech& M) {
-    size_t d = (size_t)4 * M.nrg + accw_len(M.n, M.ng) + M.n + 2 * (size_t)M.nrs + 4 * (size_t)M.nfo + M.n + M.ntb;
-    return (d + 1) & ~(size_t)1;   // 16-byte multiple
+constexpr int SP_BYTES = 3 * 64 * 8;
+__host__ __device__ inline int fod_off_bytes(int nrg) { return (16 * nrg + 15) & ~15; }
+__host__ __device__ inline int skd_off_bytes(int nrg, int nfo) { return fod_off_bytes(nrg) + 32 * nfo; }
+__host__ __device__ inline int rblock_bytes(int nrg, int nfo, int nrs) {
+    return SP_BYTES + skd_off_bytes(nrg, nfo) + 16 * nrs;
 }
-__device__ __forceinline__ Smem carve(double* p, const DevMech& M) {
-    Smem s;
-    s.kf = p; p += M.nrg;
-    s.kr = p; p += M.nrg;
-    s.jpre = p; p += M.nrg;
-    s.jdm = p; p += M.nrg;
-    s.accw = p; p += accw_len(M.n, M.ng);
-    s.accs = p; p += M.n;
-    s.ks = p; p += M.nrs;
-    s.sk = p; p += M.nrs;
-    s.k0 = p; p += M.nfo;
-    s.lfc = p; p += M.nfo;
-    s.tcc = p; p += M.nfo;
-    s.tnn = p; p += M.nfo;
-    s.conc = p; p += M.n;
-    s.mc = p;
-    return s;
+__device__ __forceinline__ RView rview(char* spbase, const DevMech& M) {
+    RView r;
+    r.sp = reinterpret_cast<double*>(spbase);
+    r.rxd = reinterpret_cast<double*>(spbase + SP_BYTES);
+    r.fod = reinterpret_cast<double*>(spbase + SP_BYTES + M.fod_off);
+    r.skd = reinterpret_cast<double*>(spbase + SP_BYTES + M.skd_off);
+    return r;
 }
 
-// fp64 LDS accumulate, relaxed, wavefront scope (ds_add_f64; deterministic inside one wave)
+// fp64 LDS accumulate, relaxed, wavefront scope (ds_add_f64, no return)
 __device__ __forceinline__ void lds_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 // acc[k] += nu_k * v over a reaction's net-stoichiometry scatter list (3 packed words)
-__device__ __forceinline__ void scatter(double* acc, const uint32_t* sc, double v) {
-    const uint32_t w0 = sc[0], w1 = sc[1], w2 = sc[2];
+__device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, double v) {
     const int cnt = (w1 >> 16) & 255;
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
@@ -233,84 +188,86 @@ __device__ __forceinline__ void scatter(double* acc, const uint32_t* sc, double 
     }
 }
 
-// stage the packed tables (all threads of the workgroup), then barrier
-__device__ __forceinline__ void stage_tables(const DevMech& M, uint32_t* dst) {
-    const int t = threadIdx.x, nt = blockDim.x;
-    for (int i = t; i < M.tab_words; i += nt) dst[i] = M.tab[i];
-    double* dd = reinterpret_cast<double*>(dst + M.tab_words);
-    for (int i = t; i < M.ntbe; i += nt) dd[i] = M.tab_d[i];
+// stage the table image (all threads of the workgroup), then barrier
+__device__ __forceinline__ void stage_tables(const DevMech& M, char* dst) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const int nv = M.img_bytes / 16;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) d[i] = M.img[i];
     __syncthreads();
 }
 
-// T-only constants (src/BatchReactor.jl:14-17: T is a per-reactor constant)
-__device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, Smem& S, double T, int lane) {
+// T-only constants (src/BatchReactor.jl:14-17: T is a per-reactor constant); g/RT scratch in accw
+__device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, const RView& R, double T, int lane) {
     const double lT = log(T);
-    for (int k = lane; k < M.ng; k += WAVE) {   // g/RT per species into qb (scratch)
+    double* grt = R.sp + 64;
+#pragma unroll 1
+    for (int k = lane; k < M.ng; k += WAVE) {
         const double* c = M.nasa + 15 * k;
         const double* a = (T < c[0]) ? c + 8 : c + 1;
         const double h = a[0] + a[1] * T / 2 + a[2] * T * T / 3 + a[3] * T * T * T / 4 + a[4] * T * T * T * T / 5 + a[5] / T;
         const double s = a[0] * lT + a[1] * T + a[2] * T * T / 2 + a[3] * T * T * T / 3 + a[4] * T * T * T * T / 4 + a[6];
-        S.accw[k] = h - s;
+        grt[k] = h - s;
     }
     wave_sync();
     const double RT = R_GAS * T;
+#pragma unroll 1
     for (int r = lane; r < M.nrg; r += WAVE) {
-        const uint32_t info = tb.rx_info[r];
-        const double A = M.g_arr[r], b = M.g_arr[M.nrg + r], EoR = M.g_arr[2 * M.nrg + r];
-        const double kf = A * exp(b * lT - EoR / T);
+        const uint32_t* rec = tb.rx + RX_WORDS * r;
+        const uint32_t info = rec[2];
+        const double* gp = M.g_par + 4 * r;
+        const double kf = gp[0] * exp(gp[1] * lT - gp[2] / T);
         double kr = 0.0;
         if (gi_rev(info)) {
             double dg = 0.0;
             const int nf = gi_nf(info), nr = gi_nr(info);
-            const uint32_t fw = tb.rx_sp[r], rw = tb.rx_pr[r];
-            for (int e = 0; e < 4; ++e) if (e < nr) dg += S.accw[sp8(rw, e)];
-            for (int e = 0; e < 4; ++e) if (e < nf) dg -= S.accw[sp8(fw, e)];
+            for (int e = 0; e < 4; ++e) if (e < nr) dg += grt[sp8(rec[1], e)];
+            for (int e = 0; e < 4; ++e) if (e < nf) dg -= grt[sp8(rec[0], e)];
             double Kc = exp(-dg) * pow(M.p_std / RT, (double)M.g_dnu[r]);
-            Kc *= M.g_kcs[r];
+            Kc *= gp[3];
             kr = kf / Kc;
         }
-        S.kf[r] = kf;
-        S.kr[r] = kr;
+        R.rxd[2 * r] = kf;
+        R.rxd[2 * r + 1] = kr;
         if (gi_tb(info) == 2) {
             const int fi = gi_foidx(info);
-            const double A0 = M.fo_low[fi], b0 = M.fo_low[M.nfo + fi], E0 = M.fo_low[2 * M.nfo + fi];
-            S.k0[fi] = A0 * exp(b0 * lT - E0 / T);
+            const double* fp = M.fo_par + 8 * fi;
+            double* fo = R.fod + 4 * fi;
+            fo[0] = fp[0] * exp(fp[1] * lT - fp[2] / T);
             double fcv = 1.0;
-            if (M.fo_ntroe[fi]) {
-                const double ta = M.fo_troe[fi], t3 = M.fo_troe[M.nfo + fi], t1 = M.fo_troe[2 * M.nfo + fi];
-                const double t2 = M.fo_troe[3 * M.nfo + fi];
-                fcv = (1 - ta) * exp(-T / t3) + ta * exp(-T / t1);
-                if (M.fo_ntroe[fi] == 4) fcv += exp(-t2 / T);
+            if (gi_troe(info)) {
+                fcv = (1 - fp[3]) * exp(-T / fp[4]) + fp[3] * exp(-T / fp[5]);
+                if (gi_troe(info) == 4) fcv += exp(-fp[6] / T);
             }
             const double lfc = log10(fcv);
-            S.lfc[fi] = lfc;
-            S.tcc[fi] = -0.4 - 0.67 * lfc;
-            S.tnn[fi] = 0.75 - 1.27 * lfc;
+            fo[1] = lfc;
+            fo[2] = -0.4 - 0.67 * lfc;
+            fo[3] = 0.75 - 1.27 * lfc;
         }
     }
+#pragma unroll 1
     for (int r = lane; r < M.nrs; r += WAVE) {
-        const uint32_t info = tb.sx_info[r];
-        const double A = M.s_arr[r], b = M.s_arr[M.nrs + r], Ea = M.s_arr[2 * M.nrs + r];
+        const uint32_t info = tb.sx[SX_WORDS * r + 4];
+        const double* sp = M.s_par + 4 * r;
         double k;
-        if (si_stick(info)) k = A * sqrt(RT / (2 * M_PI * M.molwt[si_gas(info)]));
-        else k = A * pow(T, b) * exp(-Ea / RT);
-        S.ks[r] = k;
+        if (si_stick(info)) k = sp[0] * sqrt(RT / (2 * M_PI * sp[3]));
+        else k = sp[0] * pow(T, sp[1]) * exp(-sp[2] / RT);
+        R.skd[2 * r] = k;
     }
     wave_sync();
 }
 
-// falloff: fac = Pr/(1+Pr)*F and d fac / d[M]
+// falloff: fac = Pr/(1+Pr)*F and d fac / d[M] (CHEMKIN Lindemann / Troe)
 template <bool WANT_D>
-__device__ __forceinline__ void falloff(const DevMech& M, const Smem& S, int r, int fi, double Mc, double& fac,
+__device__ __forceinline__ void falloff(const double* fo, bool troe, double kinf, double Mc, double& fac,
                                         double& dfac) {
-    const double kinf = S.kf[r], k0 = S.k0[fi];
+    const double k0 = fo[0];
     const double Pr = k0 * Mc / kinf;
     double F = 1.0, g = 0.0;
-    if (M.fo_ntroe[fi]) {
+    if (troe) {
         const double Prs = Pr > 1e-300 ? Pr : 1e-300;
-        const double lfc = S.lfc[fi];
+        const double lfc = fo[1];
         const double L = log10(Prs);
-        const double cc = S.tcc[fi], nn = S.tnn[fi];
+        const double cc = fo[2], nn = fo[3];
         const double den = nn - 0.14 * (L + cc);
         const double f1 = (L + cc) / den;
         const double lF = lfc / (1 + f1 * f1);
@@ -324,68 +281,82 @@ __device__ __forceinline__ void falloff(const DevMech& M, const Smem& S, int r, 
     if (WANT_D) dfac = (F / ((1 + Pr) * (1 + Pr)) + F * g / (1 + Pr)) * (k0 / kinf);
 }
 
-// third-body concentrations [M]_t = Ctot + sum (eff-1) c   (conc in S.conc)
-__device__ __forceinline__ void third_body(const DevMech& M, const Tab& tb, Smem& S, double Ctot, int lane) {
-    for (int t = lane; t < M.ntb; t += WAVE) {
-        double s = Ctot;
-        const int e = tb.tb_ptr[t + 1];
-        for (int i = tb.tb_ptr[t]; i < e; ++i) s += tb.tb_de[i] * S.conc[tb.tb_sp[i]];
-        S.mc[t] = s;
+// third-body concentration of one reaction: [M] = Ctot + sum (eff-1) c over its list
+__device__ __forceinline__ double third_body(const Tab& tb, const double* conc, uint32_t w3, double Ctot) {
+    double s = Ctot;
+    const int b = w3 & 0xFFFFF, e = b + (int)(w3 >> 20);
+#pragma unroll 1
+    for (int i = b; i < e; ++i) {
+        const char* ent = tb.tbe + 16 * i;
+        s += *reinterpret_cast<const double*>(ent + 8) * conc[*reinterpret_cast<const int*>(ent)];
     }
+    return s;
 }
 
 // rates of progress, accumulated straight into the per-species production sums:
 // accw[k] += nu_kr q_r (gas reactions), accs[k] += nu_kr q_r (surface reactions)
-__device__ __forceinline__ void production(const DevMech& M, const Tab& tb, Smem& S, double RT, int lane) {
+__device__ __forceinline__ void production(const DevMech& M, const Tab& tb, const RView& R, double RT, double Ctot,
+                                           int lane) {
     const bool xm = (M.conv & 2) != 0;
+    const double* conc = R.sp;
+    double* accw = R.sp + 64;
+    double* accs = R.sp + 128;
+#pragma unroll 1
     for (int r = lane; r < M.nrg; r += WAVE) {
-        const uint32_t info = tb.rx_info[r], fw = tb.rx_sp[r], rw = tb.rx_pr[r];
+        const uint4 ra = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
+        const uint4 rb = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
+        const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
+        const uint32_t info = ra.z;
         const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
         double Pf = 1.0, Pb = 1.0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) if (e < nf) Pf *= S.conc[sp8(fw, e)];
+        for (int e = 0; e < 4; ++e) if (e < nf) Pf *= conc[sp8(ra.x, e)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) if (e < nr) Pb *= S.conc[sp8(rw, e)];
-        double D = S.kf[r] * Pf - S.kr[r] * Pb;
-        if (tbk == 1) D *= S.mc[gi_tbidx(info)];
-        else if (tbk == 2) {
-            const double Mc = S.mc[gi_tbidx(info)];
-            double fac, dfac;
-            falloff<false>(M, S, r, gi_foidx(info), Mc, fac, dfac);
-            D *= fac;
-            if (xm) D *= Mc;
+        for (int e = 0; e < 4; ++e) if (e < nr) Pb *= conc[sp8(ra.y, e)];
+        double D = k.x * Pf - k.y * Pb;
+        if (tbk) {
+            const double Mc = third_body(tb, conc, ra.w, Ctot);
+            if (tbk == 1) D *= Mc;
+            else {
+                double fac, dfac;
+                falloff<false>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, k.x, Mc, fac, dfac);
+                D *= fac;
+                if (xm) D *= Mc;
+            }
         }
-        scatter(S.accw, tb.rx_sc + 3 * r, D);
+        scatter(accw, rb.x, rb.y, rb.z, D);
     }
+#pragma unroll 1
     for (int r = lane; r < M.nrs; r += WAVE) {
-        const uint32_t info = tb.sx_info[r];
-        const int nf = si_nf(info), np = si_np(info), nc = si_ncov(info);
+        const uint32_t* rec = tb.sx + SX_WORDS * r;
+        const uint32_t info = rec[4];
+        const int nf = si_nf(info), nc = si_ncov(info);
         const bool stick = si_stick(info);
-        double k = S.ks[r];
+        double k = R.skd[2 * r];
         if (nc) {
-            const uint32_t cs = M.s_cov_sp[r];
+            const uint32_t cs = rec[5];
             double s = 0.0;
-            for (int j = 0; j < 4; ++j) if (j < nc) s += M.s_cov_eps[j * M.nrs + r] * S.conc[sp8(cs, j)];
+            for (int j = 0; j < 4; ++j) if (j < nc) s += tb.sxe[4 * r + j] * conc[sp8(cs, j)];
             k *= exp(-s / RT);
         }
         double P = 1.0;
-        const uint32_t w0 = tb.sx_sp[2 * r], w1 = tb.sx_sp[2 * r + 1];
 #pragma unroll
         for (int e = 0; e < 6; ++e) if (e < nf) {
-            const int sp = e < 4 ? sp8(w0, e) : sp8(w1, e - 4);
-            if (sp < M.ng || stick) P *= S.conc[sp];
-            else P *= S.conc[sp] * M.G / M.sigma[sp];
+            const int sp = e < 4 ? sp8(rec[0], e) : sp8(rec[1], e - 4);
+            if (sp < M.ng || stick) P *= conc[sp];
+            else P *= conc[sp] * M.G / tb.sigma[sp];
         }
-        scatter(S.accs, tb.sx_sc + 3 * r, k * P);
+        scatter(accs, rec[6], rec[7], rec[8], k * P);
     }
 }
 
-// residual! (src/BatchReactor.jl:312-376) for component `lane`; returns du_lane and the
-// diagnosed pressure (save_data semantics).
-__device__ __noinline__ double rhs(const DevMech& M, const Tab& tb, Smem& S, double T, double Asv, double Asv_th,
-                                    double u, int lane, double Mk, double* p_out) {
+// residual! (src/BatchReactor.jl:312-376) for component `lane`; returns du_lane and writes the
+// diagnosed pressure to *p_out (save_data semantics).
+__device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RView& R, double T, double Asv,
+                                      double Asv_th, double u, int lane, double* p_out) {
     const bool gas = lane < M.ng;
     const bool act = lane < M.n;
+    const double Mk = tb.molwt[lane];
     const double rho = wave_sum(gas ? u : 0.0);                 // :326
     const double Y = u / rho;                                    // :328
     const double t = gas ? Y / Mk : 0.0;
@@ -394,114 +365,131 @@ __device__ __noinline__ double rhs(const DevMech& M, const Tab& tb, Smem& S, dou
     const double Mb = wave_sum(gas ? x * Mk : 0.0);              // average_molwt
     const double p = rho * R_GAS * T / Mb;                       // :338 / :353
     const double c = gas ? p * x / (R_GAS * T) : u;
-    if (act) { S.conc[lane] = c; S.accw[lane] = 0.0; S.accs[lane] = 0.0; }
+    if (act) { R.sp[lane] = c; R.sp[64 + lane] = 0.0; R.sp[128 + lane] = 0.0; }
     const double Ctot = M.ntb ? wave_sum(gas ? c : 0.0) : 0.0;
     wave_sync();
-    third_body(M, tb, S, Ctot, lane);
+    production(M, tb, R, R_GAS * T, Ctot, lane);                 // :344, :355
     wave_sync();
-    production(M, tb, S, R_GAS * T, lane);                      // :344, :355
-    wave_sync();
-    const double w = act ? S.accw[lane] : 0.0;
-    const double s = act ? S.accs[lane] : 0.0;
+    const double w = act ? R.sp[64 + lane] : 0.0;
+    const double s = act ? R.sp[128 + lane] : 0.0;
     wave_sync();
     if (lane == 0) *p_out = p;
     if (gas) return (s * Asv + w) * Mk;                          // :345, :363-370
     if (!act) return 0.0;
-    return s * Asv_th * M.sigma[lane] / M.G;                    // :367 / :370
+    return s * Asv_th * tb.sigma[lane] / M.G;                   // :367 / :370
 }
 
 // analytic Jacobian d(du)/du, written column by column to the per-reactor workspace
 // Jsave[j*64 + k] = J[k][j] (coalesced). Column j is built from the reactions whose rate
-// depends on component j (host-built column lists, incl. third-body reactions).
-__device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, Smem& S, double T, double Asv,
-                                         double Asv_th, double u, int lane, double Mk, double* Jsave) {
+// depends on component j (host-built column lists, incl. third-body reactions). The
+// per-reaction multipliers (pre, D*dpre/d[M]) go through a global scratch `jscr` (2 per gas
+// reaction), written by the reaction's lane and read back by any lane with L1-bypassing loads.
+__device__ __forceinline__ double ld_l2(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const RView& R, double T, double Asv,
+                                         double Asv_th, double u, int lane, double* Jsave, double* jscr) {
+    Jsave = launder(Jsave);
+    jscr = launder(jscr);
     const bool gas = lane < M.ng;
     const bool act = lane < M.n;
     const double RT = R_GAS * T;
     const bool xm = (M.conv & 2) != 0;
+    const double Mk = tb.molwt[lane];
+    double* conc = R.sp;
+    double* accw = R.sp + 64;
+    double* accs = R.sp + 128;
     const double c = gas ? u / Mk : u;                           // c_k = u_k/M_k = p x_k/(RT)
-    if (act) S.conc[lane] = c;
+    if (act) conc[lane] = c;
     const double Ctot = M.ntb ? wave_sum(gas ? c : 0.0) : 0.0;
     wave_sync();
-    third_body(M, tb, S, Ctot, lane);
-    wave_sync();
+#pragma unroll 1
     for (int r = lane; r < M.nrg; r += WAVE) {                   // per-reaction multipliers
-        const uint32_t info = tb.rx_info[r], fw = tb.rx_sp[r], rw = tb.rx_pr[r];
+        const uint32_t* rec = tb.rx + RX_WORDS * r;
+        const uint32_t info = rec[2];
         const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
+        const double kf = R.rxd[2 * r], kr = R.rxd[2 * r + 1];
         double Pf = 1.0, Pb = 1.0;
-        for (int e = 0; e < 4; ++e) if (e < nf) Pf *= S.conc[sp8(fw, e)];
-        for (int e = 0; e < 4; ++e) if (e < nr) Pb *= S.conc[sp8(rw, e)];
-        const double D = S.kf[r] * Pf - S.kr[r] * Pb;
+        for (int e = 0; e < 4; ++e) if (e < nf) Pf *= conc[sp8(rec[0], e)];
+        for (int e = 0; e < 4; ++e) if (e < nr) Pb *= conc[sp8(rec[1], e)];
+        const double D = kf * Pf - kr * Pb;
         double pre = 1.0, coefM = 0.0;
-        if (tbk == 1) { pre = S.mc[gi_tbidx(info)]; coefM = 1.0; }
-        else if (tbk == 2) {
-            const double Mc = S.mc[gi_tbidx(info)];
-            double fac, dfac;
-            falloff<true>(M, S, r, gi_foidx(info), Mc, fac, dfac);
-            pre = fac * (xm ? Mc : 1.0);
-            coefM = dfac * (xm ? Mc : 1.0) + (xm ? fac : 0.0);
+        if (tbk) {
+            const double Mc = third_body(tb, conc, rec[3], Ctot);
+            if (tbk == 1) { pre = Mc; coefM = 1.0; }
+            else {
+                double fac, dfac;
+                falloff<true>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, kf, Mc, fac, dfac);
+                pre = fac * (xm ? Mc : 1.0);
+                coefM = dfac * (xm ? Mc : 1.0) + (xm ? fac : 0.0);
+            }
         }
-        S.jpre[r] = pre;
-        S.jdm[r] = D * coefM;
+        jscr[2 * r] = pre;
+        jscr[2 * r + 1] = D * coefM;
     }
+#pragma unroll 1
     for (int r = lane; r < M.nrs; r += WAVE) {
-        const uint32_t info = tb.sx_info[r];
-        const int nc = si_ncov(info);
-        double k = S.ks[r];
+        const uint32_t* rec = tb.sx + SX_WORDS * r;
+        const int nc = si_ncov(rec[4]);
+        double k = R.skd[2 * r];
         if (nc) {
-            const uint32_t cs = M.s_cov_sp[r];
             double s = 0.0;
-            for (int j = 0; j < 4; ++j) if (j < nc) s += M.s_cov_eps[j * M.nrs + r] * S.conc[sp8(cs, j)];
+            for (int j = 0; j < 4; ++j) if (j < nc) s += tb.sxe[4 * r + j] * conc[sp8(rec[5], j)];
             k *= exp(-s / RT);
         }
-        S.sk[r] = k;
+        R.skd[2 * r + 1] = k;
     }
+    __builtin_amdgcn_s_waitcnt(0);   // scratch stores complete before other lanes read them
+    wave_sync();
+#pragma unroll 1
     for (int j = 0; j < M.n; ++j) {
-        if (act) { S.accw[lane] = 0.0; S.accs[lane] = 0.0; }
+        if (act) { accw[lane] = 0.0; accs[lane] = 0.0; }
         wave_sync();
         const int cb = M.col_ptr[j], ce = M.col_ptr[j + 1];
+#pragma unroll 1
         for (int i = cb + lane; i < ce; i += WAVE) {
             const int rr = M.col_rx[i];
             if (rr < M.nrg) {
                 const int r = rr;
-                const uint32_t info = tb.rx_info[r], fw = tb.rx_sp[r], rw = tb.rx_pr[r];
+                const uint32_t* rec = tb.rx + RX_WORDS * r;
+                const uint32_t info = rec[2];
                 const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
-                const double pre = S.jpre[r];
+                const double pre = ld_l2(jscr + 2 * r);
                 double d = 0.0;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) if (e < nf && sp8(fw, e) == j) {
-                    double pr = S.kf[r];
+                for (int e = 0; e < 4; ++e) if (e < nf && sp8(rec[0], e) == j) {
+                    double pr = R.rxd[2 * r];
 #pragma unroll
-                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nf) pr *= S.conc[sp8(fw, e2)];
+                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nf) pr *= conc[sp8(rec[0], e2)];
                     d += pre * pr;
                 }
 #pragma unroll
-                for (int e = 0; e < 4; ++e) if (e < nr && sp8(rw, e) == j) {
-                    double pr = S.kr[r];
+                for (int e = 0; e < 4; ++e) if (e < nr && sp8(rec[1], e) == j) {
+                    double pr = R.rxd[2 * r + 1];
 #pragma unroll
-                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= S.conc[sp8(rw, e2)];
+                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= conc[sp8(rec[1], e2)];
                     d -= pre * pr;
                 }
-                if (tbk && j < M.ng) d += S.jdm[r] * M.tb_eff[gi_tbidx(info) * M.n + j];
-                scatter(S.accw, tb.rx_sc + 3 * r, d);
+                if (tbk && j < M.ng) d += ld_l2(jscr + 2 * r + 1) * M.tb_eff[gi_tbidx(info) * M.n + j];
+                scatter(accw, rec[4], rec[5], rec[6], d);
             } else {
                 const int r = rr - M.nrg;
-                const uint32_t info = tb.sx_info[r];
-                const int nf = si_nf(info), np = si_np(info), nc = si_ncov(info);
+                const uint32_t* rec = tb.sx + SX_WORDS * r;
+                const uint32_t info = rec[4];
+                const int nf = si_nf(info), nc = si_ncov(info);
                 const bool stick = si_stick(info);
-                const double k = S.sk[r];
-                const uint32_t w0 = tb.sx_sp[2 * r], w1 = tb.sx_sp[2 * r + 1];
+                const double k = R.skd[2 * r + 1];
                 double cv[6], dc[6];
                 int sp[6];
 #pragma unroll
                 for (int e = 0; e < 6; ++e) {
-                    sp[e] = e < nf ? (e < 4 ? sp8(w0, e) : sp8(w1, e - 4)) : -1;
+                    sp[e] = e < nf ? (e < 4 ? sp8(rec[0], e) : sp8(rec[1], e - 4)) : -1;
                     cv[e] = 1.0; dc[e] = 0.0;
                     if (e < nf) {
                         const int s = sp[e];
-                        if (s < M.ng) { cv[e] = S.conc[s]; dc[e] = 1.0 / M.molwt[s]; }
-                        else if (stick) { cv[e] = S.conc[s]; dc[e] = 1.0; }
-                        else { cv[e] = S.conc[s] * M.G / M.sigma[s]; dc[e] = M.G / M.sigma[s]; }
+                        if (s < M.ng) { cv[e] = conc[s]; dc[e] = 1.0 / tb.molwt[s]; }
+                        else if (stick) { cv[e] = conc[s]; dc[e] = 1.0; }
+                        else { cv[e] = conc[s] * M.G / tb.sigma[s]; dc[e] = M.G / tb.sigma[s]; }
                     }
                 }
                 double d = 0.0;
@@ -517,107 +505,177 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, Smem& 
 #pragma unroll
                     for (int e = 0; e < 6; ++e) if (e < nf) P *= cv[e];
                     const double q = k * P;
-                    const uint32_t cs = M.s_cov_sp[r];
-                    for (int jj = 0; jj < 4; ++jj) if (jj < nc && sp8(cs, jj) == j)
-                        d += q * (-M.s_cov_eps[jj * M.nrs + r] / RT);
+                    for (int jj = 0; jj < 4; ++jj) if (jj < nc && sp8(rec[5], jj) == j)
+                        d += q * (-tb.sxe[4 * r + jj] / RT);
                 }
-                scatter(S.accs, tb.sx_sc + 3 * r, d);
+                scatter(accs, rec[6], rec[7], rec[8], d);
             }
         }
         wave_sync();
-        const double w = act ? S.accw[lane] : 0.0;
-        const double s = act ? S.accs[lane] : 0.0;
+        const double w = act ? accw[lane] : 0.0;
+        const double s = act ? accs[lane] : 0.0;
         double v;
-        if (gas) v = (j < M.ng ? Mk * w / M.molwt[j] : 0.0) + Mk * Asv * s;
-        else v = Asv_th * M.sigma[act ? lane : 0] / M.G * s;
+        if (gas) v = (j < M.ng ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * s;
+        else v = Asv_th * tb.sigma[lane] / M.G * s;
         Jsave[j * WAVE + lane] = act ? v : 0.0;
         wave_sync();
     }
 }
 
 // ------------------------------------------------------------------------------------
-// LU of I - gamma*J, row-per-lane (SUNDIALS denseGETRF semantics: partial pivoting on max
-// |a_ik|, multipliers mult = 1/a_kk, a_ij -= a_kj * l_ik), without physical row swaps.
-// Rolled over k: each lane keeps the live part of its row left-aligned in registers
-// (a[0] = current column) and shifts it by one per step, so the code stays a few KB (the
-// fully unrolled form is ~NMAX^2 blocks and thrashes the instruction cache). Finished
-// columns go to LU[k*64 + lane]. Returns fail (0 or k+1 for a zero pivot) and this lane's
-// pivot step in `pstep` (-> the row order).
+// LU of A = I - gamma*J, row-per-lane (SUNDIALS denseGETRF semantics: partial pivoting on the
+// first max |a_ik| in row order, multipliers l_ik = a_ik / a_kk, a_ij -= l_ik a_kj), without
+// physical row swaps. Column k of the factors goes to LU[k*64 + lane] (coalesced):
+//   rows still to be pivoted: the multiplier l; the pivot row of step k: 1/a_kk (reciprocal, so
+//   the solve multiplies); rows pivoted earlier: their U entry in column k.
+// Pivot search: wave max of |a_k| over the remaining rows (DPP on the two dwords + v_max_f64),
+// then the lowest lane holding that value (ballot + ff1) = the first max in row order.
 // ------------------------------------------------------------------------------------
-template <int NMAX>
-__device__ __noinline__ int lu_factor_mem(const double* __restrict__ J, double* __restrict__ LU, double gamma, int n,
-                                          int lane, int* pstep_out) {
+__device__ __forceinline__ double wave_max_pos(double v) {   // v >= 0 or -1 on idle lanes
+    v = fmax(v, dppd<0xB1>(v));
+    v = fmax(v, dppd<0x4E>(v));
+    v = fmax(v, dppd<0x141>(v));
+    v = fmax(v, dppd<0x140>(v));
+    return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
+}
+
+// right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
+// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors to LU, rank-1
+// update of the live columns, shift by one (the loop over k stays rolled).
+template <int W>
+__device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep, int& fail,
+                                            double* __restrict__ LU) {
     constexpr int CH = 8;
-    static_assert(NMAX % CH == 0, "NMAX must be a multiple of 8");
-    double a[NMAX];
-#pragma unroll
-    for (int j = 0; j < NMAX; ++j) {
-        a[j] = -gamma * J[j * WAVE + lane];
-        if (j == lane) a[j] += 1.0;
-    }
-    int pstep = (lane < n) ? -1 : NMAX + 1;
-    int fail = 0;
-    for (int k = 0; k < n; ++k) {
+    static_assert(W % CH == 0, "W must be a multiple of 8");
+#pragma unroll 1
+    for (int k = k0; k < k1; ++k) {
         const double v = (pstep < 0) ? fabs(a[0]) : -1.0;
-        const int p = wave_argmax(v);
+        const double vmax = wave_max_pos(v);
+        const unsigned long long hit = __ballot(pstep < 0 && v == vmax);
+        const int p = hit ? (int)__builtin_ctzll(hit) : 0;
         const double piv = bcast(a[0], p);
         if (piv == 0.0 && !fail) fail = k + 1;
-        if (lane == p) pstep = k;
+        const double rinv = 1.0 / piv;
+        const bool isp = (lane == p);
+        if (isp) pstep = k;
         const bool rem = pstep < 0;
-        const double mult = 1.0 / piv;
-        const double l = a[0] * mult;
-        LU[k * WAVE + lane] = rem ? l : a[0];
-        const int live = n - k;                 // columns k..n-1 are live; a[0..live-1]
+        const double l = rem ? a[0] * rinv : 0.0;
+        LU[k * WAVE + lane] = rem ? l : (isp ? rinv : a[0]);
+        const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
 #pragma unroll
-        for (int c = 0; c < NMAX; c += CH) {
+        for (int c = 0; c < W; c += CH) {
             if (c < live) {
 #pragma unroll
                 for (int i = 0; i < CH; ++i) {
                     const int j = c + i;
-                    if (j + 1 < NMAX) {
-                        const double apj = bcast(a[j + 1], p);
-                        a[j] = rem ? a[j + 1] - apj * l : a[j + 1];
-                    } else {
-                        a[j] = 0.0;
-                    }
+                    if (j + 1 < W) a[j] = fma(-bcast(a[j + 1], p), l, a[j + 1]);
+                    else a[j] = 0.0;
                 }
             }
         }
     }
-    for (int k = n; k < NMAX; ++k) LU[k * WAVE + lane] = (k == lane) ? 1.0 : 0.0;
-    *pstep_out = pstep;
+}
+
+// LU in two column panels of P = 32 (registers: 2P per lane, not 2n): panel 1 = columns
+// 0..P-1 factored right-looking; panel 2 = columns P..n-1 first receives the P updates of panel
+// 1 (left-looking: multipliers re-read from LU, pivot-row values broadcast from the panel-2
+// registers of the pivot lane, in step order), then is factored right-looking. The arithmetic
+// is exactly that of the unblocked right-looking LU. Returns 0 or k+1 for a zero pivot.
+template <int NMAX>
+__device__ __forceinline__ int lu_factor(const double* __restrict__ J, double* __restrict__ LU, double gamma, int n,
+                                         int lane, int& pstep_out) {
+    constexpr int P = NMAX < 32 ? NMAX : 32;
+    constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
+    J = launder(J);
+    LU = launder(LU);
+    lane = launder_v(lane);
+    int pstep = (lane < n) ? -1 : 1024;
+    int fail = 0;
+    const int n1 = n < P ? n : P;
+    {
+        double a[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const double jv = (j < n) ? J[j * WAVE + lane] : 0.0;
+            a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
+        }
+        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, fail, LU);
+    }
+    if (NMAX > P && n > P) {
+        double b[W2];
+#pragma unroll
+        for (int j = 0; j < W2; ++j) {
+            const int col = P + j;
+            const double jv = (col < n) ? J[col * WAVE + lane] : 0.0;
+            b[j] = ((col == lane) ? 1.0 : 0.0) - gamma * jv;
+        }
+        constexpr int CH = 8;
+        double cur[CH], nxt[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) cur[i] = LU[i * WAVE + lane];
+#pragma unroll 1
+        for (int kb = 0; kb < P; kb += CH) {
+            if (kb + CH < P) {
+#pragma unroll
+                for (int i = 0; i < CH; ++i) nxt[i] = LU[(kb + CH + i) * WAVE + lane];
+            }
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const int k = kb + i;
+                const unsigned long long m = __ballot(pstep == k);
+                const int p = (int)__builtin_ctzll(m);
+                const double l = (pstep > k) ? cur[i] : 0.0;
+#pragma unroll
+                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), l, b[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
+        }
+        lu_rl_steps<W2>(b, P, n, n, lane, pstep, fail, LU);
+    }
+    pstep_out = pstep;
     return fail;
 }
 
-__device__ __forceinline__ int pivot_lane(int pstep, int k) {
-    const unsigned long long m = __ballot(pstep == k);
-    return __builtin_ctzll(m);
+// row order after factorization: lane i of the solve works on the pivot row of step i, i.e.
+// original row perm[i] (perm = inverse of pstep); lanes >= n map to themselves
+__device__ __forceinline__ int pivot_perm(int pstep, int lane, int n) {
+    const int dst = (lane < n) ? pstep : lane;
+    return __builtin_amdgcn_ds_permute(dst * 4, lane);
+}
+__device__ __forceinline__ double lane_pull(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src * 4, (int)(b & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_ds_bpermute(src * 4, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// solve (LU) x = b with the factors stored column-major per lane: LU[k*64 + lane] = a_lane[k].
-// Rolled over chunks of 8 columns; the next chunk's loads are issued before the current
-// chunk's dependent chain, so the chain does not wait on memory.
+// solve (I - gamma J) x = b with the factors of lu_factor. `perm` from pivot_perm; b and the
+// returned x are in natural component order (lane k <-> component k). The factor columns are
+// read with a per-lane row address (perm), one 512-B segment per column, 8 columns in flight.
 template <int NMAX>
-__device__ __noinline__ double lu_solve_mem(const double* __restrict__ LU, int n, int lane, int pstep, double b) {
+__device__ __forceinline__ double lu_solve(const double* __restrict__ LU, int n, int lane, int perm, double b) {
     constexpr int CH = 8;
-    double r = b;
+    LU = launder(LU);
+    double r = lane_pull(b, perm);                 // P b
+    const double* col = LU + perm;
     double cur[CH], nxt[CH];
     const int nch = (n + CH - 1) / CH;
 #pragma unroll
-    for (int i = 0; i < CH; ++i) cur[i] = LU[i * WAVE + lane];
-    for (int cb = 0; cb < nch; ++cb) {
+    for (int i = 0; i < CH; ++i) cur[i] = col[i * WAVE];
+#pragma unroll 1
+    for (int cb = 0; cb < nch; ++cb) {            // forward: L y = P b (unit lower)
         const int c = cb * CH;
         if (cb + 1 < nch) {
 #pragma unroll
-            for (int i = 0; i < CH; ++i) nxt[i] = LU[(c + CH + i) * WAVE + lane];
+            for (int i = 0; i < CH; ++i) nxt[i] = col[(c + CH + i) * WAVE];
         }
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
             const int k = c + i;
             if (k < n) {
-                const int p = pivot_lane(pstep, k);
-                const double yk = bcast(r, p);
-                if (pstep > k && lane < n) r = r - cur[i] * yk;
+                const double yk = bcast(r, k);
+                if (lane > k) r = fma(-cur[i], yk, r);
             }
         }
 #pragma unroll
@@ -625,32 +683,27 @@ __device__ __noinline__ double lu_solve_mem(const double* __restrict__ LU, int n
     }
     const int c_last = (nch - 1) * CH;
 #pragma unroll
-    for (int i = 0; i < CH; ++i) cur[i] = LU[(c_last + i) * WAVE + lane];
-    for (int cb = nch - 1; cb >= 0; --cb) {
+    for (int i = 0; i < CH; ++i) cur[i] = col[(c_last + i) * WAVE];
+#pragma unroll 1
+    for (int cb = nch - 1; cb >= 0; --cb) {       // backward: U x = y
         const int c = cb * CH;
         if (cb > 0) {
 #pragma unroll
-            for (int i = 0; i < CH; ++i) nxt[i] = LU[(c - CH + i) * WAVE + lane];
+            for (int i = 0; i < CH; ++i) nxt[i] = col[(c - CH + i) * WAVE];
         }
 #pragma unroll
         for (int i = CH - 1; i >= 0; --i) {
             const int k = c + i;
             if (k < n) {
-                const int p = pivot_lane(pstep, k);
-                if (lane == p) r = r / cur[i];
-                const double xk = bcast(r, p);
-                if (pstep < k) r = r - cur[i] * xk;
+                if (lane == k) r *= cur[i];       // 1/u_kk
+                const double xk = bcast(r, k);
+                if (lane < k) r = fma(-cur[i], xk, r);
             }
         }
 #pragma unroll
         for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
     }
-    // lane p holds x_{pstep(p)}: push it to lane pstep(p)
-    const int dst = (lane < n) ? pstep : lane;
-    const long long bits = __double_as_longlong(r);
-    const int lo = __builtin_amdgcn_ds_permute(dst * 4, (int)(bits & 0xffffffffLL));
-    const int hi = __builtin_amdgcn_ds_permute(dst * 4, (int)(bits >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    return (lane < n) ? r : 0.0;
 }
 
 }  // namespace brhip
