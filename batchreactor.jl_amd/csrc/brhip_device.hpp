@@ -624,7 +624,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J, double* _
                 const int k = kb + i;
                 const unsigned long long m = __ballot(pstep == k);
                 const int p = (int)__builtin_ctzll(m);
-                const double l = (pstep > k) ? cur[i] : 0.0;
+                const double l = ((pstep < 0 || pstep > k) && lane < n) ? cur[i] : 0.0;   // rows not yet pivoted at k
 #pragma unroll
                 for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), l, b[j]);
             }
