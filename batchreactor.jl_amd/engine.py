@@ -51,6 +51,7 @@ class Engine:
         _lib.check(L.br_mech_create(C.byref(desc), device, C.byref(h)))
         self.h = h
         self.n, self.ng, self.ns = mech.n, mech.ng, mech.ns
+        self.nmax = 16 if self.n <= 16 else 32 if self.n <= 32 else 56 if self.n <= 56 else 64   # kernel tile
 
     def close(self):
         if getattr(self, "h", None):
