@@ -69,8 +69,9 @@ __host__ __device__ inline size_t reactor_bytes(const DevMech& M) {
 }
 __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return M.img_bytes + rpb * reactor_bytes(M); }
 // per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn)
+__host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(2 * nmax + 1) * WAVE; }   // Lc, Uc, D
 __host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
-    return (size_t)2 * nmax * WAVE + (((size_t)2 * nrg + 63) / 64) * 64;
+    return (size_t)nmax * WAVE + lu_ws_doubles(nmax) + (((size_t)2 * nrg + 63) / 64) * 64;
 }
 
 struct WaveCtx {
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
     double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
     double* LUsave = Jsave + NMAX * WAVE;
-    double* jscr = LUsave + NMAX * WAVE;
+    double* jscr = LUsave + lu_ws_doubles(NMAX);
     CtlArgs a;
     a.rtol = o.rtol; a.atol = o.atol; a.hmax_inv = o.hmax_inv; a.ufac = o.ufac;
     a.max_steps = o.max_steps; a.trace_cap = o.trace_cap; a.trace = trace; a.rid = rid; a.n = n;
@@ -742,7 +743,7 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
     const bool act = lane < M.n;
     const double u = act ? U[(size_t)rid * M.n + lane] : 0.0;
     double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);
-    jacobian(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + 2 * NMAX * WAVE);
+    jacobian(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * WAVE + lu_ws_doubles(NMAX));
     if (act) {
         double* row = J + ((size_t)rid * M.n + lane) * M.n;
 #pragma unroll
@@ -1229,7 +1230,7 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     const int rid = blockIdx.x;
     if (rid >= N) return;
     const int lane = threadIdx.x;
-    double* Jt = ws + (size_t)rid * 2 * NMAX * WAVE;
+    double* Jt = ws + (size_t)rid * (NMAX * WAVE + lu_ws_doubles(NMAX));
     double* LU = Jt + NMAX * WAVE;
     for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1255,7 +1256,7 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     HIPCHK(hipMalloc(&dg, (size_t)N * 8));
     HIPCHK(hipMalloc(&db, (size_t)N * n * 8));
     HIPCHK(hipMalloc(&dx, (size_t)N * n * 8));
-    HIPCHK(hipMalloc(&dws, (size_t)N * 2 * nmax * WAVE * 8));
+    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * WAVE + lu_ws_doubles(nmax)) * 8));
     HIPCHK(hipMalloc(&df, (size_t)N * 4));
     HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));

@@ -135,10 +135,12 @@ __device__ __forceinline__ double wave_max(double v) {
 // opaque copy of a uniform pointer: addresses derived from it cannot be hoisted out of the
 // integrator's main loop (otherwise LICM keeps ~NMAX 64-bit column addresses live across the
 // whole loop and the kernel spills)
+// (the result is an explicit global-address-space pointer: global_load/store, not flat_*)
+#define BR_GLOBAL __attribute__((address_space(1)))
 template <class T>
-__device__ __forceinline__ T* launder(T* p) {
+__device__ __forceinline__ BR_GLOBAL T* launder(T* p) {
     asm volatile("" : "+s"(p));
-    return p;
+    return (BR_GLOBAL T*)p;
 }
 // opaque copy of a per-lane value (stops LICM from hoisting lane-dependent constants such as
 // the identity-matrix entries of I - gamma*J out of the main loop)
@@ -384,13 +386,13 @@ __device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RVi
 // depends on component j (host-built column lists, incl. third-body reactions). The
 // per-reaction multipliers (pre, D*dpre/d[M]) go through a global scratch `jscr` (2 per gas
 // reaction), written by the reaction's lane and read back by any lane with L1-bypassing loads.
-__device__ __forceinline__ double ld_l2(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ double ld_l2(const BR_GLOBAL double* p) {
+    return __hip_atomic_load((const double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const RView& R, double T, double Asv,
-                                         double Asv_th, double u, int lane, double* Jsave, double* jscr) {
-    Jsave = launder(Jsave);
-    jscr = launder(jscr);
+                                         double Asv_th, double u, int lane, double* Jsave_, double* jscr_) {
+    BR_GLOBAL double* Jsave = launder(Jsave_);
+    BR_GLOBAL double* jscr = launder(jscr_);
     const bool gas = lane < M.ng;
     const bool act = lane < M.n;
     const double RT = R_GAS * T;
@@ -525,9 +527,11 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
 // ------------------------------------------------------------------------------------
 // LU of A = I - gamma*J, row-per-lane (SUNDIALS denseGETRF semantics: partial pivoting on the
 // first max |a_ik| in row order, multipliers l_ik = a_ik / a_kk, a_ij -= l_ik a_kj), without
-// physical row swaps. Column k of the factors goes to LU[k*64 + lane] (coalesced):
-//   rows still to be pivoted: the multiplier l; the pivot row of step k: 1/a_kk (reciprocal, so
-//   the solve multiplies); rows pivoted earlier: their U entry in column k.
+// physical row swaps. The factors are stored for a mask-free solve, per original row (lane):
+//   Lc[k][row] = l_row,k if the row was still unpivoted at step k, else 0;
+//   Uc[k][row] = u_row,k / u_row,row if the row was pivoted before step k, else 0 (unit-diagonal
+//                U' = D^-1 U);  D[row] = 1 / u_row,row.
+// Columns n..roundup8(n)-1 of Lc/Uc are written as zeros, so the solve needs no k < n tests.
 // Pivot search: wave max of |a_k| over the remaining rows (DPP on the two dwords + v_max_f64),
 // then the lowest lane holding that value (ballot + ff1) = the first max in row order.
 // ------------------------------------------------------------------------------------
@@ -538,13 +542,18 @@ __device__ __forceinline__ double wave_max_pos(double v) {   // v >= 0 or -1 on 
     v = fmax(v, dppd<0x140>(v));
     return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
 }
+struct LUWs {   // factor workspace (global), columns of 64 lanes
+    BR_GLOBAL double* Lc;
+    BR_GLOBAL double* Uc;
+    BR_GLOBAL double* D;
+};
 
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
-// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors to LU, rank-1
+// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors, rank-1
 // update of the live columns, shift by one (the loop over k stays rolled).
 template <int W>
-__device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep, int& fail,
-                                            double* __restrict__ LU) {
+__device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
+                                            double& dinv, int& fail, const LUWs& F) {
     constexpr int CH = 8;
     static_assert(W % CH == 0, "W must be a multiple of 8");
 #pragma unroll 1
@@ -557,10 +566,11 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
         if (piv == 0.0 && !fail) fail = k + 1;
         const double rinv = 1.0 / piv;
         const bool isp = (lane == p);
-        if (isp) pstep = k;
-        const bool rem = pstep < 0;
+        const bool rem = (pstep < 0) && !isp;
+        if (isp) { pstep = k; dinv = rinv; }
         const double l = rem ? a[0] * rinv : 0.0;
-        LU[k * WAVE + lane] = rem ? l : (isp ? rinv : a[0]);
+        F.Lc[k * WAVE + lane] = l;
+        F.Uc[k * WAVE + lane] = (pstep >= 0 && !isp) ? a[0] * dinv : 0.0;
         const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
 #pragma unroll
         for (int c = 0; c < W; c += CH) {
@@ -578,18 +588,20 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
 
 // LU in two column panels of P = 32 (registers: 2P per lane, not 2n): panel 1 = columns
 // 0..P-1 factored right-looking; panel 2 = columns P..n-1 first receives the P updates of panel
-// 1 (left-looking: multipliers re-read from LU, pivot-row values broadcast from the panel-2
+// 1 (left-looking: multipliers re-read from Lc, pivot-row values broadcast from the panel-2
 // registers of the pivot lane, in step order), then is factored right-looking. The arithmetic
 // is exactly that of the unblocked right-looking LU. Returns 0 or k+1 for a zero pivot.
 template <int NMAX>
-__device__ __forceinline__ int lu_factor(const double* __restrict__ J, double* __restrict__ LU, double gamma, int n,
+__device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
                                          int lane, int& pstep_out) {
     constexpr int P = NMAX < 32 ? NMAX : 32;
     constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
-    J = launder(J);
-    LU = launder(LU);
+    const BR_GLOBAL double* J = launder(J_);
+    BR_GLOBAL double* wsg = launder(ws);
+    const LUWs F{wsg, wsg + NMAX * WAVE, wsg + 2 * NMAX * WAVE};
     lane = launder_v(lane);
     int pstep = (lane < n) ? -1 : 1024;
+    double dinv = 0.0;
     int fail = 0;
     const int n1 = n < P ? n : P;
     {
@@ -599,7 +611,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J, double* _
             const double jv = (j < n) ? J[j * WAVE + lane] : 0.0;
             a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
         }
-        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, fail, LU);
+        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F);
     }
     if (NMAX > P && n > P) {
         double b[W2];
@@ -612,27 +624,30 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J, double* _
         constexpr int CH = 8;
         double cur[CH], nxt[CH];
 #pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = LU[i * WAVE + lane];
+        for (int i = 0; i < CH; ++i) cur[i] = F.Lc[i * WAVE + lane];
 #pragma unroll 1
         for (int kb = 0; kb < P; kb += CH) {
             if (kb + CH < P) {
 #pragma unroll
-                for (int i = 0; i < CH; ++i) nxt[i] = LU[(kb + CH + i) * WAVE + lane];
+                for (int i = 0; i < CH; ++i) nxt[i] = F.Lc[(kb + CH + i) * WAVE + lane];
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) {
                 const int k = kb + i;
                 const unsigned long long m = __ballot(pstep == k);
                 const int p = (int)__builtin_ctzll(m);
-                const double l = ((pstep < 0 || pstep > k) && lane < n) ? cur[i] : 0.0;   // rows not yet pivoted at k
 #pragma unroll
-                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), l, b[j]);
+                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), cur[i], b[j]);
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
         }
-        lu_rl_steps<W2>(b, P, n, n, lane, pstep, fail, LU);
+        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F);
     }
+    const int npad = (n + 7) & ~7;
+#pragma unroll 1
+    for (int k = n; k < npad; ++k) { F.Lc[k * WAVE + lane] = 0.0; F.Uc[k * WAVE + lane] = 0.0; }
+    F.D[lane] = dinv;
     pstep_out = pstep;
     return fail;
 }
@@ -650,59 +665,51 @@ __device__ __forceinline__ double lane_pull(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// solve (I - gamma J) x = b with the factors of lu_factor. `perm` from pivot_perm; b and the
-// returned x are in natural component order (lane k <-> component k). The factor columns are
-// read with a per-lane row address (perm), one 512-B segment per column, 8 columns in flight.
+// one triangular sweep over the zero-padded factor columns col[k*64 + perm] in chunks of 8
+// (forward: k ascending, backward: descending): r -= col_k * r[k]. Two register buffers
+// alternate, so each chunk's loads are issued a full chunk ahead of their use and no register
+// rotation (which would force a wait on the prefetch) is needed.
+template <bool FWD>
+__device__ __forceinline__ void tri_chunk(const double (&v)[8], int c, double& r) {
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+        const int i = FWD ? ii : 7 - ii;
+        r = fma(-v[i], bcast(r, c + i), r);
+    }
+}
+template <bool FWD>
+__device__ __forceinline__ void tri_load(double (&v)[8], const BR_GLOBAL double* __restrict__ col, int c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = col[(c + i) * WAVE];
+}
+template <bool FWD>
+__device__ __forceinline__ double tri_sweep(const BR_GLOBAL double* __restrict__ col, int nch, double r) {
+    double A[8], B[8];
+    auto cidx = [&](int t) { return FWD ? t * 8 : (nch - 1 - t) * 8; };
+    tri_load<FWD>(A, col, cidx(0));
+    if (nch > 1) tri_load<FWD>(B, col, cidx(1));
+#pragma unroll 1
+    for (int t = 0; t < nch; t += 2) {
+        tri_chunk<FWD>(A, cidx(t), r);
+        if (t + 2 < nch) tri_load<FWD>(A, col, cidx(t + 2));
+        if (t + 1 < nch) {
+            tri_chunk<FWD>(B, cidx(t + 1), r);
+            if (t + 3 < nch) tri_load<FWD>(B, col, cidx(t + 3));
+        }
+    }
+    return r;
+}
+
+// solve (I - gamma J) x = b with the factors of lu_factor: L y = P b, y' = D^-1 y, U' x = y'.
+// `perm` from pivot_perm; b and the returned x are in natural component order.
 template <int NMAX>
-__device__ __forceinline__ double lu_solve(const double* __restrict__ LU, int n, int lane, int perm, double b) {
-    constexpr int CH = 8;
-    LU = launder(LU);
+__device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n, int lane, int perm, double b) {
+    const BR_GLOBAL double* wsg = launder(ws);
+    const int nch = (n + 7) >> 3;
     double r = lane_pull(b, perm);                 // P b
-    const double* col = LU + perm;
-    double cur[CH], nxt[CH];
-    const int nch = (n + CH - 1) / CH;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) cur[i] = col[i * WAVE];
-#pragma unroll 1
-    for (int cb = 0; cb < nch; ++cb) {            // forward: L y = P b (unit lower)
-        const int c = cb * CH;
-        if (cb + 1 < nch) {
-#pragma unroll
-            for (int i = 0; i < CH; ++i) nxt[i] = col[(c + CH + i) * WAVE];
-        }
-#pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            const int k = c + i;
-            if (k < n) {
-                const double yk = bcast(r, k);
-                if (lane > k) r = fma(-cur[i], yk, r);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
-    }
-    const int c_last = (nch - 1) * CH;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) cur[i] = col[(c_last + i) * WAVE];
-#pragma unroll 1
-    for (int cb = nch - 1; cb >= 0; --cb) {       // backward: U x = y
-        const int c = cb * CH;
-        if (cb > 0) {
-#pragma unroll
-            for (int i = 0; i < CH; ++i) nxt[i] = col[(c - CH + i) * WAVE];
-        }
-#pragma unroll
-        for (int i = CH - 1; i >= 0; --i) {
-            const int k = c + i;
-            if (k < n) {
-                if (lane == k) r *= cur[i];       // 1/u_kk
-                const double xk = bcast(r, k);
-                if (lane < k) r = fma(-cur[i], xk, r);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
-    }
+    r = tri_sweep<true>(wsg + perm, nch, r);       // forward, unit lower
+    r *= wsg[2 * NMAX * WAVE + perm];              // D^-1
+    r = tri_sweep<false>(wsg + NMAX * WAVE + perm, nch, r);   // backward, unit upper
     return (lane < n) ? r : 0.0;
 }
 
