@@ -698,13 +698,15 @@ __global__ __launch_bounds__(256) void k_rates(DevMech M, int N, int rpb, const 
     double c = 0.0;
     if (lane < M.ng) c = p * X[(size_t)rid * M.ng + lane] / (R_GAS * T);
     else if (lane < M.n) c = TH ? TH[(size_t)rid * M.ns + (lane - M.ng)] : 0.0;
-    if (lane < M.n) { S.sp[lane] = c; S.sp[64 + lane] = 0.0; S.sp[128 + lane] = 0.0; }
+    if (lane < M.n) { S.sp[SP_CONC + lane] = c; S.sp[SP_ACCW + lane] = 0.0; S.sp[SP_ACCS + lane] = 0.0; }
     const double Ctot = wave_sum(lane < M.ng ? c : 0.0);
     wave_sync();
-    production(M, W.tb, S, R_GAS * T, Ctot, lane);
+    third_body_sets(M, W.tb, S.sp, Ctot, lane);
     wave_sync();
-    const double w = lane < M.n ? S.sp[64 + lane] : 0.0;
-    const double s = lane < M.n ? S.sp[128 + lane] : 0.0;
+    production(M, W.tb, S, R_GAS * T, lane);
+    wave_sync();
+    const double w = lane < M.n ? S.sp[SP_ACCW + lane] : 0.0;
+    const double s = lane < M.n ? S.sp[SP_ACCS + lane] : 0.0;
     if (lane < M.ng) W_[(size_t)rid * M.ng + lane] = w;
     if (SD && lane < M.n) SD[(size_t)rid * M.n + lane] = s;
 }
@@ -824,9 +826,9 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     M.ng = ng; M.ns = ns; M.n = n; M.nrg = nrg; M.nrs = nrs; M.conv = d->conv;
     M.p_std = d->p_std > 0 ? d->p_std : 1e5;
     M.G = d->site_density * 1e4;
-    auto pack4 = [](const int* v, int cnt) {
+    auto pack4 = [](const int* v, int cnt, int pad = 255) {
         uint32_t w = 0;
-        for (int e = 0; e < 4; ++e) w |= (uint32_t)(e < cnt ? (v[e] & 255) : 255) << (8 * e);
+        for (int e = 0; e < 4; ++e) w |= (uint32_t)(e < cnt ? (v[e] & 255) : pad) << (8 * e);
         return w;
     };
     // net-stoichiometry scatter list of a reaction: up to 6 (species, nu != 0) pairs packed in
@@ -867,16 +869,18 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     std::vector<uint32_t> rx(RX_WORDS * (size_t)nrg, 0);
     std::vector<double> gpar(4 * (size_t)std::max(nrg, 1), 0.0), fopar(8 * (size_t)std::max(nfo, 1), 0.0);
     std::vector<int> gdnu(std::max(nrg, 1), 0);
-    std::vector<std::pair<int, double>> tbe;       // (species, eff - 1)
-    std::vector<double> tbeff;                     // dense [ntb][n]
+    std::vector<std::pair<int, double>> tbe;       // (species, eff - 1), per set
+    std::vector<std::vector<double>> sets;         // distinct efficiency rows
+    std::vector<uint32_t> tbs;                     // per set: start | count << 20
+    std::vector<double> tbeff;                     // dense [nset][n]
     int tbi = 0, foi = 0;
     for (int i = 0; i < nrg; ++i) {
         const int r = perm[i];
         const int nf = d->g_nf[r], nr = d->g_nr[r], tb = d->g_tb[r];
         if (nf > 4 || nr > 4 || nf < 1) { delete m; return fail(BR_ERR_UNSUPPORTED, "reaction with >4 entries"); }
         uint32_t* rec = &rx[RX_WORDS * (size_t)i];
-        rec[0] = pack4(d->g_f + r * 4, nf);
-        rec[1] = pack4(d->g_r + r * 4, nr);
+        rec[0] = pack4(d->g_f + r * 4, nf, SP_ONE);
+        rec[1] = pack4(d->g_r + r * 4, nr, SP_ONE);
         if (!scatter_pack(d->g_f + r * 4, nf, d->g_r + r * 4, nr, rec + 4)) {
             delete m; return fail(BR_ERR_UNSUPPORTED, "reaction touches more than 6 species");
         }
@@ -884,17 +888,22 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         gpar[4 * (size_t)i + 3] = ((d->conv & BR_CONV_KC_UNIT_SLIP) && tb != 2) ? std::pow(1e6, (double)(nr - nf)) : 1.0;
         gdnu[i] = nr - nf;
         int troe = 0, fo = 0, tbidx = 0;
-        if (tb) {
-            tbidx = tbi++;
-            const int start = (int)tbe.size();
-            for (int k = 0; k < ng; ++k) {
-                const double e = d->g_eff[(size_t)r * ng + k];
-                if (e != 1.0) tbe.push_back({k, e - 1.0});
+        if (tb) {   // third-body efficiency set (deduplicated: GRI's 41 reactions use 10 sets)
+            std::vector<double> row(d->g_eff + (size_t)r * ng, d->g_eff + (size_t)r * ng + ng);
+            int sidx = -1;
+            for (size_t q = 0; q < sets.size(); ++q) if (sets[q] == row) { sidx = (int)q; break; }
+            if (sidx < 0) {
+                sidx = (int)sets.size();
+                sets.push_back(row);
+                const int start = (int)tbe.size();
+                for (int k = 0; k < ng; ++k) if (row[k] != 1.0) tbe.push_back({k, row[k] - 1.0});
+                const int cnt = (int)tbe.size() - start;
+                if (start >= (1 << 20) || cnt >= (1 << 12)) { delete m; return fail(BR_ERR_UNSUPPORTED, "third-body list too long"); }
+                tbs.push_back((uint32_t)start | ((uint32_t)cnt << 20));
+                for (int k = 0; k < n; ++k) tbeff.push_back(k < ng ? row[k] : 0.0);
             }
-            const int cnt = (int)tbe.size() - start;
-            if (start >= (1 << 20) || cnt >= (1 << 12)) { delete m; return fail(BR_ERR_UNSUPPORTED, "third-body list too long"); }
-            rec[3] = (uint32_t)start | ((uint32_t)cnt << 20);
-            for (int k = 0; k < n; ++k) tbeff.push_back(k < ng ? d->g_eff[(size_t)r * ng + k] : 0.0);
+            tbidx = sidx;
+            tbi++;
         }
         if (tb == 2) {
             fo = foi++;
@@ -906,7 +915,8 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         rec[2] = (uint32_t)(nf | (nr << 3) | ((d->g_rev[r] ? 1 : 0) << 6) | (tb << 7) | ((troe & 7) << 9) |
                             (fo << 12) | (tbidx << 22));
     }
-    M.ntb = ntb; M.nfo = nfo; M.ntbe = (int)tbe.size();
+    M.ntb = ntb; M.nfo = nfo; M.ntbe = (int)tbe.size(); M.nset = (int)sets.size();
+    if (M.nset > 64) { delete m; return fail(BR_ERR_UNSUPPORTED, "more than 64 third-body efficiency sets"); }
     // ---- surface reactions
     std::vector<uint32_t> sx(SX_WORDS * (size_t)nrs, 0);
     std::vector<double> sxe(4 * (size_t)nrs, 0.0), spar(4 * (size_t)std::max(nrs, 1), 0.0);
@@ -963,6 +973,8 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     off += al16(32 * (size_t)nrs);
     M.tbe_off = (int)off;
     off += al16(16 * tbe.size());
+    M.tbs_off = (int)off;
+    off += al16(4 * tbs.size());
     M.img_bytes = (int)al16(off);
     std::vector<unsigned char> img(M.img_bytes, 0);
     {
@@ -973,6 +985,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         if (nrg) memcpy(img.data() + IMG_RX_OFF, rx.data(), rx.size() * 4);
         if (nrs) memcpy(img.data() + M.sx_off, sx.data(), sx.size() * 4);
         if (nrs) memcpy(img.data() + M.sxe_off, sxe.data(), sxe.size() * 8);
+        if (!tbs.empty()) memcpy(img.data() + M.tbs_off, tbs.data(), tbs.size() * 4);
         for (size_t i = 0; i < tbe.size(); ++i) {
             unsigned char* e = img.data() + M.tbe_off + 16 * i;
             const int sp = tbe[i].first;

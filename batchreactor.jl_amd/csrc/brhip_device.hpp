@@ -28,11 +28,12 @@ constexpr int WAVE = 64;
 // mechanism description (host-built)
 // ------------------------------------------------------------------------------------
 struct DevMech {
-    int ng, ns, n, nrg, nrs, ntb, nfo, ntbe, conv;
+    int ng, ns, n, nrg, nrs, ntb, nfo, ntbe, nset, conv;
     double p_std, G;              // Pa ; site density mol/m2
     const uint4* img;             // LDS table image (global copy)
     int img_bytes;                // multiple of 16
     int sx_off, sxe_off, tbe_off; // byte offsets in the image
+    int tbs_off;                  // third-body efficiency sets: one word (start | count << 20) each
     int fod_off, skd_off;         // byte offsets of FOD / SKD from the reactor's RXD base
     int rblock_bytes;             // per-reactor LDS bytes from SP start (SP + RXD + FOD + SKD)
     // init only (T-dependent constants)
@@ -42,13 +43,14 @@ struct DevMech {
     const double* fo_par;         // [nfo][8]: A0, b0, E0/R, a, T***, T*, T**, ntroe
     const double* s_par;          // [nrs][4]: A or s0, beta, Ea [J/mol], M_gas (stick)
     // Jacobian only
-    const double* tb_eff;         // [ntb][n] dense efficiencies
+    const double* tb_eff;         // [nset][n] dense efficiencies
     const int* col_ptr;           // [n+1] Jacobian column lists
     const int* col_rx;            // combined reaction index (gas r, surface nrg+r)
 };
 
-// RX record: w0 reactant species (4 x 8 bit, 255 pad), w1 product species, w2 info,
-// w3 third-body list (start | count << 20), w4..w6 net-stoichiometry scatter list, w7 pad
+// RX record: w0 reactant species (4 x 8 bit; pad = SP_ONE, a slot holding 1.0, so the
+// concentration products need no branches), w1 product species, w2 info (third-body
+// efficiency set in bits 22..31), w3 pad, w4..w6 net-stoichiometry scatter list, w7 pad
 __host__ __device__ inline int gi_nf(uint32_t v) { return v & 7; }
 __host__ __device__ inline int gi_nr(uint32_t v) { return (v >> 3) & 7; }
 __host__ __device__ inline int gi_rev(uint32_t v) { return (v >> 6) & 1; }
@@ -74,6 +76,7 @@ struct Tab {   // views of the staged table image
     const uint32_t* sx;    // SX_WORDS per surface reaction
     const double* sxe;     // 4 per surface reaction
     const char* tbe;       // 16 B per third-body entry
+    const uint32_t* tbs;   // per efficiency set: start | count << 20 into tbe
 };
 __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
     Tab t;
@@ -83,6 +86,7 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
     t.sx = reinterpret_cast<const uint32_t*>(base + M.sx_off);
     t.sxe = reinterpret_cast<const double*>(base + M.sxe_off);
     t.tbe = base + M.tbe_off;
+    t.tbs = reinterpret_cast<const uint32_t*>(base + M.tbs_off);
     return t;
 }
 
@@ -153,12 +157,15 @@ __device__ __forceinline__ int launder_v(int v) {
 // per-reactor rate workspace (LDS)
 // ------------------------------------------------------------------------------------
 struct RView {
-    double* sp;    // conc[k] = sp[k], accw[k] = sp[64+k], accs[k] = sp[128+k]
+    double* sp;    // species block: conc[k] = sp[SP_CONC+k], accw, accs, mc (see SP_* offsets)
     double* rxd;   // kf = rxd[2r], kr = rxd[2r+1]
     double* fod;   // k0, log10 Fcent, c, n per falloff reaction
     double* skd;   // k(T), k*exp(-sum eps theta/RT) (Jacobian) per surface reaction
 };
-constexpr int SP_BYTES = 3 * 64 * 8;
+// species block (doubles): conc[0..63], conc[SP_ONE] = 1.0 (pad species), accw[64], accs[64],
+// mc[64] third-body concentration per efficiency set
+constexpr int SP_CONC = 0, SP_ONE = 64, SP_ACCW = 80, SP_ACCS = 144, SP_MC = 208, SP_DOUBLES = 272;
+constexpr int SP_BYTES = SP_DOUBLES * 8;
 __host__ __device__ inline int fod_off_bytes(int nrg) { return (16 * nrg + 15) & ~15; }
 __host__ __device__ inline int skd_off_bytes(int nrg, int nfo) { return fod_off_bytes(nrg) + 32 * nfo; }
 __host__ __device__ inline int rblock_bytes(int nrg, int nfo, int nrs) {
@@ -201,7 +208,8 @@ __device__ __forceinline__ void stage_tables(const DevMech& M, char* dst) {
 // T-only constants (src/BatchReactor.jl:14-17: T is a per-reactor constant); g/RT scratch in accw
 __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, const RView& R, double T, int lane) {
     const double lT = log(T);
-    double* grt = R.sp + 64;
+    double* grt = R.sp + SP_ACCW;
+    if (lane == 0) R.sp[SP_ONE] = 1.0;
 #pragma unroll 1
     for (int k = lane; k < M.ng; k += WAVE) {
         const double* c = M.nasa + 15 * k;
@@ -283,41 +291,52 @@ __device__ __forceinline__ void falloff(const double* fo, bool troe, double kinf
     if (WANT_D) dfac = (F / ((1 + Pr) * (1 + Pr)) + F * g / (1 + Pr)) * (k0 / kinf);
 }
 
-// third-body concentration of one reaction: [M] = Ctot + sum (eff-1) c over its list
-__device__ __forceinline__ double third_body(const Tab& tb, const double* conc, uint32_t w3, double Ctot) {
-    double s = Ctot;
-    const int b = w3 & 0xFFFFF, e = b + (int)(w3 >> 20);
+// third-body concentrations of the efficiency sets: mc[s] = Ctot + sum (eff-1) c over the set's
+// list (one lane per set; the list entries are read 2 at a time so the loads overlap)
+__device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb, double* sp, double Ctot, int lane) {
+    const double* conc = sp + SP_CONC;
 #pragma unroll 1
-    for (int i = b; i < e; ++i) {
-        const char* ent = tb.tbe + 16 * i;
-        s += *reinterpret_cast<const double*>(ent + 8) * conc[*reinterpret_cast<const int*>(ent)];
+    for (int t = lane; t < M.nset; t += WAVE) {
+        const uint32_t w = tb.tbs[t];
+        const int b = w & 0xFFFFF, e = b + (int)(w >> 20);
+        double s0 = Ctot, s1 = 0.0;
+        int i = b;
+#pragma unroll 1
+        for (; i + 1 < e; i += 2) {
+            const double2 e0 = *reinterpret_cast<const double2*>(tb.tbe + 16 * i);
+            const double2 e1 = *reinterpret_cast<const double2*>(tb.tbe + 16 * (i + 1));
+            const int k0 = __double_as_longlong(e0.x) & 0xFFFF, k1 = __double_as_longlong(e1.x) & 0xFFFF;
+            s0 = fma(e0.y, conc[k0], s0);
+            s1 = fma(e1.y, conc[k1], s1);
+        }
+        if (i < e) {
+            const double2 e0 = *reinterpret_cast<const double2*>(tb.tbe + 16 * i);
+            s0 = fma(e0.y, conc[__double_as_longlong(e0.x) & 0xFFFF], s0);
+        }
+        sp[SP_MC + t] = s0 + s1;
     }
-    return s;
 }
 
 // rates of progress, accumulated straight into the per-species production sums:
 // accw[k] += nu_kr q_r (gas reactions), accs[k] += nu_kr q_r (surface reactions)
-__device__ __forceinline__ void production(const DevMech& M, const Tab& tb, const RView& R, double RT, double Ctot,
-                                           int lane) {
+__device__ __forceinline__ void production(const DevMech& M, const Tab& tb, const RView& R, double RT, int lane) {
     const bool xm = (M.conv & 2) != 0;
-    const double* conc = R.sp;
-    double* accw = R.sp + 64;
-    double* accs = R.sp + 128;
+    const double* conc = R.sp + SP_CONC;
+    double* accw = R.sp + SP_ACCW;
+    double* accs = R.sp + SP_ACCS;
 #pragma unroll 1
     for (int r = lane; r < M.nrg; r += WAVE) {
         const uint4 ra = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
         const uint4 rb = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
         const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
         const uint32_t info = ra.z;
-        const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
-        double Pf = 1.0, Pb = 1.0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) if (e < nf) Pf *= conc[sp8(ra.x, e)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) if (e < nr) Pb *= conc[sp8(ra.y, e)];
+        const int tbk = gi_tb(info);
+        // branch-free mass-action products: unused slots point at conc[SP_ONE] = 1
+        const double Pf = (conc[sp8(ra.x, 0)] * conc[sp8(ra.x, 1)]) * (conc[sp8(ra.x, 2)] * conc[sp8(ra.x, 3)]);
+        const double Pb = (conc[sp8(ra.y, 0)] * conc[sp8(ra.y, 1)]) * (conc[sp8(ra.y, 2)] * conc[sp8(ra.y, 3)]);
         double D = k.x * Pf - k.y * Pb;
         if (tbk) {
-            const double Mc = third_body(tb, conc, ra.w, Ctot);
+            const double Mc = R.sp[SP_MC + gi_tbidx(info)];
             if (tbk == 1) D *= Mc;
             else {
                 double fac, dfac;
@@ -359,21 +378,21 @@ __device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RVi
     const bool gas = lane < M.ng;
     const bool act = lane < M.n;
     const double Mk = tb.molwt[lane];
-    const double rho = wave_sum(gas ? u : 0.0);                 // :326
-    const double Y = u / rho;                                    // :328
-    const double t = gas ? Y / Mk : 0.0;
-    const double ssum = wave_sum(t);
-    const double x = gas ? t / ssum : 0.0;                       // massfrac_to_molefrac!
-    const double Mb = wave_sum(gas ? x * Mk : 0.0);              // average_molwt
-    const double p = rho * R_GAS * T / Mb;                       // :338 / :353
-    const double c = gas ? p * x / (R_GAS * T) : u;
-    if (act) { R.sp[lane] = c; R.sp[64 + lane] = 0.0; R.sp[128 + lane] = 0.0; }
-    const double Ctot = M.ntb ? wave_sum(gas ? c : 0.0) : 0.0;
+    // Y = u/rho, x = (Y/M)/sum(Y/M), p = rho R T / Mbar (:326-338 / :349-353) give the gas
+    // concentrations c_k = p x_k / (R T) = u_k / M_k exactly; p = R T sum_k c_k
+    const double c = gas ? u / Mk : u;
+    if (act) { R.sp[SP_CONC + lane] = c; R.sp[SP_ACCW + lane] = 0.0; R.sp[SP_ACCS + lane] = 0.0; }
+    const double Ctot = wave_sum(gas ? c : 0.0);
+    const double p = R_GAS * T * Ctot;
+    if (M.nset) {
+        wave_sync();
+        third_body_sets(M, tb, R.sp, Ctot, lane);
+    }
     wave_sync();
-    production(M, tb, R, R_GAS * T, Ctot, lane);                 // :344, :355
+    production(M, tb, R, R_GAS * T, lane);                       // :344, :355
     wave_sync();
-    const double w = act ? R.sp[64 + lane] : 0.0;
-    const double s = act ? R.sp[128 + lane] : 0.0;
+    const double w = act ? R.sp[SP_ACCW + lane] : 0.0;
+    const double s = act ? R.sp[SP_ACCS + lane] : 0.0;
     wave_sync();
     if (lane == 0) *p_out = p;
     if (gas) return (s * Asv + w) * Mk;                          // :345, :363-370
@@ -398,13 +417,17 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
     const double RT = R_GAS * T;
     const bool xm = (M.conv & 2) != 0;
     const double Mk = tb.molwt[lane];
-    double* conc = R.sp;
-    double* accw = R.sp + 64;
-    double* accs = R.sp + 128;
+    double* conc = R.sp + SP_CONC;
+    double* accw = R.sp + SP_ACCW;
+    double* accs = R.sp + SP_ACCS;
     const double c = gas ? u / Mk : u;                           // c_k = u_k/M_k = p x_k/(RT)
     if (act) conc[lane] = c;
-    const double Ctot = M.ntb ? wave_sum(gas ? c : 0.0) : 0.0;
+    const double Ctot = wave_sum(gas ? c : 0.0);
     wave_sync();
+    if (M.nset) {
+        third_body_sets(M, tb, R.sp, Ctot, lane);
+        wave_sync();
+    }
 #pragma unroll 1
     for (int r = lane; r < M.nrg; r += WAVE) {                   // per-reaction multipliers
         const uint32_t* rec = tb.rx + RX_WORDS * r;
@@ -417,7 +440,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
         const double D = kf * Pf - kr * Pb;
         double pre = 1.0, coefM = 0.0;
         if (tbk) {
-            const double Mc = third_body(tb, conc, rec[3], Ctot);
+            const double Mc = R.sp[SP_MC + gi_tbidx(info)];
             if (tbk == 1) { pre = Mc; coefM = 1.0; }
             else {
                 double fac, dfac;

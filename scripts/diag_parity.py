@@ -25,6 +25,13 @@ U, st = eng.integrate(T, Asv, U0, tf, rtol=rtol, atol=atol)
 Ua, sa, _ = om.integrate_batch(T, Asv, U0, tf, rtol=rtol, atol=atol, analytic_jac=True, nthreads=8)
 Ud, sd, _ = om.integrate_batch(T, Asv, U0, tf, rtol=rtol, atol=atol, analytic_jac=False, nthreads=8)
 names = pm.gas_species + [f"s{i}" for i in range(pm.ns)]
+Ut, stt, _ = om.integrate_batch(T, Asv, U0, tf, rtol=1e-10, atol=1e-14, analytic_jac=True, nthreads=8)
+for i in range(N):
+    fl = 1e-6 * np.abs(Ut[i]).max()
+    eg = np.abs(U[i] - Ut[i]) / (np.abs(Ut[i]) + fl)
+    ea = np.abs(Ua[i] - Ut[i]) / (np.abs(Ut[i]) + fl)
+    k = int(np.argmax(eg))
+    print(f"{i}: global err gpu {eg.max():.3e} ({names[k]}: gpu {U[i,k]:.6e} true {Ut[i,k]:.6e} orc {Ua[i,k]:.6e}) orc {ea.max():.3e}")
 for i in range(N):
     e = np.abs(U[i] - Ua[i]) / (1e-4 * np.abs(Ua[i]) + 100 * atol)
     e2 = np.abs(Ud[i] - Ua[i]) / (1e-4 * np.abs(Ua[i]) + 100 * atol)

@@ -98,6 +98,9 @@ def test_rhs_and_jacobian_parity(pkg, orc, gpu, case):
     T, p, x, th = _states(pm, N, 12)
     Asv = np.exp(np.random.default_rng(3).uniform(0, np.log(100), N))
     U = np.stack([pm.initial_state(T[i], p[i], x[i], th[i] if pm.ns else None) for i in range(N)])
+    # half the states get small negative entries (post-ignition solver states have them)
+    neg = np.random.default_rng(4).random(U.shape) < 0.15
+    U[N // 2:] = np.where(neg[N // 2:], -1e-3 * np.abs(U[N // 2:]), U[N // 2:])
     du = eng.rhs(T, Asv, U)
     J = eng.jacobian(T, Asv, U)
     for i in range(N):
@@ -148,34 +151,44 @@ def _global_err(X, Ut):
     return e.max(axis=1)
 
 
-@pytest.mark.parametrize("case,N,tf", [("h2o2", 32, 10.0), ("gri", 8, 10.0), ("surf", 16, 10.0)])
-def test_integrate_parity(pkg, orc, gpu, case, N, tf):
+@pytest.mark.parametrize("case,N", [("h2o2", 256), ("gri", 64), ("surf", 64)])
+def test_integrate_parity(pkg, orc, gpu, case, N):
     """Default tolerances (rtol 1e-6, atol 1e-10, src/BatchReactor.jl:141,:210), 0 -> 10 s through
-    ignition. Two CVODE runs that differ only in rounding take different step sequences after
-    ignition, and their end states then agree only to the global error of the method, which at
-    rtol 1e-6 reaches 1e-3..1e-2 on some species for the reference's own setting (oracle with CVODE's
-    DQ Jacobian, measured against an rtol-1e-10 solution). The test therefore measures every run's
-    global error against a tight-tolerance oracle solution and requires the engine's to be of the
-    same size as the oracle's: per reactor within max(20x the worse oracle error, 5e-3), and the
-    batch median within 3x the oracle's median."""
+    ignition, on a slice of the synthetic ensemble (bench inputs).
+
+    Two CVODE runs that differ only in rounding take different step sequences after ignition, and
+    their end states then agree only to the global error of the method, which at rtol 1e-6 reaches
+    1e-3..1e-2 on some species for the reference's own setting (oracle with CVODE's DQ Jacobian,
+    measured against an rtol-1e-10 solution). Past ignition some trajectories also enter
+    negative-concentration states (a few per cent of H2/O2 reactors, in the oracle as in the
+    engine, rounding-dependent). Parity is therefore statistical: every run's global error is
+    measured against a tight-tolerance oracle solution and the engine's distribution must match
+    the oracle's (median, 90th percentile, outlier fraction, runaway fraction)."""
+    from batchreactor_amd import ensemble
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
-    T, Asv, U0 = _ignition_inputs(pm, case, N, 5)
+    T, Asv, U0 = ensemble.make_inputs(pm, case, 0, N)
+    tf = 10.0
     U, st = eng.integrate(T, Asv, U0, tf)
-    assert np.all(st["status"] == 0)
-    Ua, sta, bad_a = om.integrate_batch(T, Asv, U0, tf, analytic_jac=True, nthreads=4)
-    Ud, std_, bad_d = om.integrate_batch(T, Asv, U0, tf, analytic_jac=False, nthreads=4)
-    Ut, stt, bad_t = om.integrate_batch(T, Asv, U0, tf, rtol=1e-10, atol=1e-14, analytic_jac=True, nthreads=4)
-    assert bad_a == 0 and bad_d == 0 and bad_t == 0
-    eg, ea, ed = _global_err(U, Ut), _global_err(Ua, Ut), _global_err(Ud, Ut)
-    for i in range(N):
-        assert eg[i] <= max(20 * max(ea[i], ed[i]), 5e-3), (case, i, eg[i], ea[i], ed[i])
+    Ua, sta, _ = om.integrate_batch(T, Asv, U0, tf, analytic_jac=True, nthreads=8)
+    Ud, std_, _ = om.integrate_batch(T, Asv, U0, tf, analytic_jac=False, nthreads=8)
+    Ut, stt, _ = om.integrate_batch(T, Asv, U0, tf, rtol=1e-10, atol=1e-14, analytic_jac=True, nthreads=8)
+    sg = st["status"]
+    sa = np.array([s["status"] for s in sta])
+    sd = np.array([s["status"] for s in std_])
+    assert set(np.unique(sg)) <= {0, -7}                     # success or runaway stop, nothing else
+    assert abs(np.mean(sg != 0) - np.mean(sa != 0)) <= 0.03 + 2.0 / N
+    ok = (sg == 0) & (sa == 0) & (sd == 0) & np.array([s["status"] == 0 for s in stt])
+    assert ok.sum() >= 0.9 * N
+    eg, ea, ed = _global_err(U[ok], Ut[ok]), _global_err(Ua[ok], Ut[ok]), _global_err(Ud[ok], Ut[ok])
+    eo = np.maximum(ea, ed)
     assert np.median(eg) <= 3 * np.median(ea) + 1e-7, (np.median(eg), np.median(ea))
-    # same algorithm -> the same work up to rounding-induced path differences: after ignition
-    # single reactors can take quite different step sequences (both within tolerance), so the
-    # step count is compared over the batch
-    ng_, no_ = float(np.sum(st["nsteps"])), float(sum(s["nsteps"] for s in sta))
-    assert abs(ng_ - no_) <= 0.15 * no_, (ng_, no_)
+    assert np.percentile(eg, 90) <= 3 * np.percentile(eo, 90) + 1e-4, (np.percentile(eg, 90), np.percentile(eo, 90))
+    assert np.mean(eg > 5e-2) <= 2 * np.mean(eo > 5e-2) + 3.0 / N, (np.mean(eg > 5e-2), np.mean(eo > 5e-2))
+    # same algorithm -> the same work up to rounding-induced path differences
+    ng_ = float(np.sum(st["nsteps"][ok]))
+    no_ = float(sum(sta[i]["nsteps"] for i in np.nonzero(ok)[0]))
+    assert abs(ng_ - no_) <= 0.1 * no_, (ng_, no_)
 
 
 @pytest.mark.parametrize("case,N", [("h2o2", 16), ("gri", 4), ("surf", 8)])
