@@ -916,18 +916,28 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
                             (fo << 12) | (tbidx << 22));
     }
     M.ntb = ntb; M.nfo = nfo; M.ntbe = (int)tbe.size(); M.nset = (int)sets.size();
+    M.nu4 = 0;
+    for (int r = 0; r < nrg; ++r) if (d->g_nf[r] > 3 || d->g_nr[r] > 3) M.nu4 = 1;
     if (M.nset > 64) { delete m; return fail(BR_ERR_UNSUPPORTED, "more than 64 third-body efficiency sets"); }
     // ---- surface reactions
     std::vector<uint32_t> sx(SX_WORDS * (size_t)nrs, 0);
-    std::vector<double> sxe(4 * (size_t)nrs, 0.0), spar(4 * (size_t)std::max(nrs, 1), 0.0);
+    std::vector<double> sxe(SXE_DOUBLES * (size_t)nrs, 0.0), spar(4 * (size_t)std::max(nrs, 1), 0.0);
     for (int r = 0; r < nrs; ++r) {
         const int nf = d->s_nf[r], np = d->s_np[r], nc = d->s_ncov[r];
         if (nf > 6 || np > 6 || nc > 4) { delete m; return fail(BR_ERR_UNSUPPORTED, "surface reaction too large"); }
         uint32_t* rec = &sx[SX_WORDS * (size_t)r];
         int e6[6];
-        for (int e = 0; e < 6; ++e) e6[e] = e < nf ? d->s_f[r * 6 + e] : 255;
+        for (int e = 0; e < 6; ++e) e6[e] = e < nf ? d->s_f[r * 6 + e] : SP_ONE;
         rec[0] = pack4(e6, 4);
-        rec[1] = pack4(e6 + 4, 2);
+        rec[1] = pack4(e6 + 4, 2, SP_ONE);
+        // constant site factor of the rate: Gamma/sigma per surface reactant (concentration
+        // theta*Gamma/sigma), 1 for gas reactants and for sticking reactions (theta only)
+        double fold = 1.0;
+        for (int e = 0; e < nf; ++e) {
+            const int sp = d->s_f[r * 6 + e];
+            if (sp >= ng && !d->s_stick[r]) fold *= M.G / (d->sigma ? d->sigma[sp - ng] : 1.0);
+        }
+        sxe[SXE_DOUBLES * (size_t)r + 4] = fold;
         int p6[6];
         for (int e = 0; e < 6; ++e) p6[e] = e < np ? d->s_p[r * 6 + e] : 255;
         rec[2] = pack4(p6, 4);
@@ -936,7 +946,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
             delete m; return fail(BR_ERR_UNSUPPORTED, "surface reaction touches more than 6 species");
         }
         int cs[4] = {0, 0, 0, 0};
-        for (int c = 0; c < nc; ++c) { cs[c] = d->s_cov_sp[r * 4 + c]; sxe[4 * (size_t)r + c] = d->s_cov_eps[r * 4 + c]; }
+        for (int c = 0; c < nc; ++c) { cs[c] = d->s_cov_sp[r * 4 + c]; sxe[SXE_DOUBLES * (size_t)r + c] = d->s_cov_eps[r * 4 + c]; }
         rec[5] = pack4(cs, 4);
         int g = -1;
         for (int e = 0; e < nf; ++e) if (d->s_f[r * 6 + e] < ng) g = d->s_f[r * 6 + e];
@@ -970,7 +980,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     M.sx_off = (int)off;
     off += al16(SX_WORDS * 4 * (size_t)nrs);
     M.sxe_off = (int)off;
-    off += al16(32 * (size_t)nrs);
+    off += al16(8 * SXE_DOUBLES * (size_t)nrs);
     M.tbe_off = (int)off;
     off += al16(16 * tbe.size());
     M.tbs_off = (int)off;

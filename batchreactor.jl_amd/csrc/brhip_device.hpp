@@ -29,6 +29,7 @@ constexpr int WAVE = 64;
 // ------------------------------------------------------------------------------------
 struct DevMech {
     int ng, ns, n, nrg, nrs, ntb, nfo, ntbe, nset, conv;
+    int nu4;                      // some gas reaction has 4 reactants or 4 products
     double p_std, G;              // Pa ; site density mol/m2
     const uint4* img;             // LDS table image (global copy)
     int img_bytes;                // multiple of 16
@@ -66,7 +67,7 @@ __host__ __device__ inline int si_stick(uint32_t v) { return (v >> 6) & 1; }
 __host__ __device__ inline int si_ncov(uint32_t v) { return (v >> 7) & 7; }
 __host__ __device__ inline int si_gas(uint32_t v) { return (v >> 10) & 255; }
 __host__ __device__ inline int sp8(uint32_t w, int e) { return (w >> (8 * e)) & 255; }
-constexpr int RX_WORDS = 8, SX_WORDS = 12;
+constexpr int RX_WORDS = 8, SX_WORDS = 12, SXE_DOUBLES = 8;
 constexpr int IMG_RX_OFF = 1024;
 
 struct Tab {   // views of the staged table image
@@ -74,7 +75,7 @@ struct Tab {   // views of the staged table image
     const double* sigma;   // [64]
     const uint32_t* rx;    // RX_WORDS per gas reaction
     const uint32_t* sx;    // SX_WORDS per surface reaction
-    const double* sxe;     // 4 per surface reaction
+    const double* sxe;     // SXE_DOUBLES per surface reaction: coverage eps[4], site factor, pad
     const char* tbe;       // 16 B per third-body entry
     const uint32_t* tbs;   // per efficiency set: start | count << 20 into tbe
 };
@@ -109,6 +110,14 @@ __device__ __forceinline__ double bcast(double v, int lane) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// broadcast through the LDS crossbar (ds_bpermute, no LDS memory): runs on the LDS pipe, so a
+// stream of independent broadcasts (the LU's pivot-row elements) costs no VALU issue slots
+__device__ __forceinline__ double bcast_x(double v, int lane_addr4) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(lane_addr4, (int)(b & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_ds_bpermute(lane_addr4, (int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ __forceinline__ double uni(double v) {
@@ -192,7 +201,7 @@ __device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, u
         if (e < cnt) {
             const int k = e < 4 ? sp8(w0, e) : sp8(w1, e - 4);
             const int nu = ((int)(w2 << (28 - 4 * e))) >> 28;   // sign-extended nibble
-            lds_add(&acc[k], nu == 1 ? v : (nu == -1 ? -v : nu * v));
+            lds_add(&acc[k], (double)nu * v);                    // exact for small integer nu
         }
     }
 }
@@ -331,9 +340,11 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb, cons
         const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
         const uint32_t info = ra.z;
         const int tbk = gi_tb(info);
-        // branch-free mass-action products: unused slots point at conc[SP_ONE] = 1
-        const double Pf = (conc[sp8(ra.x, 0)] * conc[sp8(ra.x, 1)]) * (conc[sp8(ra.x, 2)] * conc[sp8(ra.x, 3)]);
-        const double Pb = (conc[sp8(ra.y, 0)] * conc[sp8(ra.y, 1)]) * (conc[sp8(ra.y, 2)] * conc[sp8(ra.y, 3)]);
+        // branch-free mass-action products: unused slots point at conc[SP_ONE] = 1; mechanisms
+        // with at most 3 reactants / products per reaction (M.nu4 == 0, GRI) skip the 4th slot
+        double Pf = (conc[sp8(ra.x, 0)] * conc[sp8(ra.x, 1)]) * conc[sp8(ra.x, 2)];
+        double Pb = (conc[sp8(ra.y, 0)] * conc[sp8(ra.y, 1)]) * conc[sp8(ra.y, 2)];
+        if (M.nu4) { Pf *= conc[sp8(ra.x, 3)]; Pb *= conc[sp8(ra.y, 3)]; }
         double D = k.x * Pf - k.y * Pb;
         if (tbk) {
             const double Mc = R.sp[SP_MC + gi_tbidx(info)];
@@ -350,23 +361,19 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb, cons
 #pragma unroll 1
     for (int r = lane; r < M.nrs; r += WAVE) {
         const uint32_t* rec = tb.sx + SX_WORDS * r;
-        const uint32_t info = rec[4];
-        const int nf = si_nf(info), nc = si_ncov(info);
-        const bool stick = si_stick(info);
-        double k = R.skd[2 * r];
+        const int nc = si_ncov(rec[4]);
+        const double* xe = tb.sxe + SXE_DOUBLES * r;
+        // k(T) times the constant site factors (Gamma/sigma per surface reactant, 1 for sticking)
+        double k = R.skd[2 * r] * xe[4];
         if (nc) {
             const uint32_t cs = rec[5];
             double s = 0.0;
-            for (int j = 0; j < 4; ++j) if (j < nc) s += tb.sxe[4 * r + j] * conc[sp8(cs, j)];
+            for (int j = 0; j < 4; ++j) if (j < nc) s += xe[j] * conc[sp8(cs, j)];
             k *= exp(-s / RT);
         }
-        double P = 1.0;
-#pragma unroll
-        for (int e = 0; e < 6; ++e) if (e < nf) {
-            const int sp = e < 4 ? sp8(rec[0], e) : sp8(rec[1], e - 4);
-            if (sp < M.ng || stick) P *= conc[sp];
-            else P *= conc[sp] * M.G / tb.sigma[sp];
-        }
+        // branch-free product over up to 6 reactants (pad slots = conc[SP_ONE] = 1)
+        const double P = ((conc[sp8(rec[0], 0)] * conc[sp8(rec[0], 1)]) * (conc[sp8(rec[0], 2)] * conc[sp8(rec[0], 3)])) *
+                         (conc[sp8(rec[1], 0)] * conc[sp8(rec[1], 1)]);
         scatter(accs, rec[6], rec[7], rec[8], k * P);
     }
 }
@@ -459,7 +466,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
         double k = R.skd[2 * r];
         if (nc) {
             double s = 0.0;
-            for (int j = 0; j < 4; ++j) if (j < nc) s += tb.sxe[4 * r + j] * conc[sp8(rec[5], j)];
+            for (int j = 0; j < 4; ++j) if (j < nc) s += tb.sxe[SXE_DOUBLES * r + j] * conc[sp8(rec[5], j)];
             k *= exp(-s / RT);
         }
         R.skd[2 * r + 1] = k;
@@ -531,7 +538,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
                     for (int e = 0; e < 6; ++e) if (e < nf) P *= cv[e];
                     const double q = k * P;
                     for (int jj = 0; jj < 4; ++jj) if (jj < nc && sp8(rec[5], jj) == j)
-                        d += q * (-tb.sxe[4 * r + jj] / RT);
+                        d += q * (-tb.sxe[SXE_DOUBLES * r + jj] / RT);
                 }
                 scatter(accs, rec[6], rec[7], rec[8], d);
             }
