@@ -17,6 +17,10 @@
 #include "../../include/brhip.h"
 #include "brhip_device.hpp"
 
+#ifndef BR_PHASE_CLOCKS
+#define BR_PHASE_CLOCKS 0   // per-phase shader-clock counters in br_stats (diagnostic build: libbrhip_diag.so)
+#endif
+
 using namespace brhip;
 
 namespace {
@@ -57,6 +61,10 @@ struct Ctl {
     int nst, nfe, nsetups, nje, nni, ncfn, netf, nstlp, nstlj;
     int ncf, nef, nstloc, status, m_it, convfail, count1, phase;
     int callSetup, jbad, jcur_nls, hnewOK, newj;
+    // per-launch constants (here rather than in registers: they are read once per step)
+    double a_rtol, a_atol, a_hmax_inv, a_ufac;
+    double* a_trace;
+    int a_max_steps, a_trace_cap, a_rid, a_n;
 };
 constexpr int CTL_BYTES = (sizeof(Ctl) + 15) / 16 * 16;
 enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, acor, ewt, tempv, y
@@ -109,12 +117,22 @@ __device__ __forceinline__ double wrms_l(double v, double ewt, int lane, int n) 
     return uni(sqrt(wave_sum(t * t) / n));
 }
 
-struct CtlArgs {   // per-launch constants the controller needs
+struct CtlArgs {   // per-launch constants the controller needs, read (uniform) from the LDS controller
     double rtol, atol, hmax_inv, ufac;
-    int max_steps, trace_cap;
     double* trace;
-    int rid, n;
+    int max_steps, trace_cap, rid, n;
 };
+__device__ __forceinline__ CtlArgs load_args(LCtl* C) {
+    CtlArgs a;
+    a.rtol = ud(C->a_rtol); a.atol = ud(C->a_atol); a.hmax_inv = ud(C->a_hmax_inv); a.ufac = ud(C->a_ufac);
+    const volatile __attribute__((address_space(3))) unsigned long long& tp =
+        *reinterpret_cast<volatile __attribute__((address_space(3))) unsigned long long*>(&C->a_trace);
+    const unsigned long long tv = tp;
+    const unsigned lo = (unsigned)uni((int)(tv & 0xffffffffull)), hi = (unsigned)uni((int)(tv >> 32));
+    a.trace = reinterpret_cast<double*>(((unsigned long long)hi << 32) | lo);
+    a.max_steps = ui(C->a_max_steps); a.trace_cap = ui(C->a_trace_cap); a.rid = ui(C->a_rid); a.n = ui(C->a_n);
+    return a;
+}
 
 // cvSet (BDF coefficients l[], tq[], gamma) for the current q, h, tau
 __device__ __forceinline__ void cv_set(LCtl* C) {
@@ -291,7 +309,8 @@ __device__ __forceinline__ void begin_step(LCtl* C, LDbl* V, int lane, const Ctl
 // Controller, part 1: after the RHS value f = F(y) of this lane is known.
 // Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
-__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, const CtlArgs a, double* rhs_out) {
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, double* rhs_out) {
+    const CtlArgs a = load_args(C);
     const int n = a.n;
     const bool act = lane < n;
     C->nfe = ui(C->nfe) + 1;
@@ -388,7 +407,8 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, 
 // Controller, part 2: after the linear solve (delta = this lane's Newton correction) or after
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
-__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double delta, int lu_fail, const CtlArgs a) {
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double delta, int lu_fail) {
+    const CtlArgs a = load_args(C);
     const int n = a.n;
     const bool act = lane < n;
     const double ewt = V[V_EWT * WAVE + lane];
@@ -591,9 +611,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
     double* LUsave = Jsave + NMAX * WAVE;
     double* jscr = LUsave + lu_ws_doubles(NMAX);
-    CtlArgs a;
-    a.rtol = o.rtol; a.atol = o.atol; a.hmax_inv = o.hmax_inv; a.ufac = o.ufac;
-    a.max_steps = o.max_steps; a.trace_cap = o.trace_cap; a.trace = trace; a.rid = rid; a.n = n;
+    C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
+    C->a_max_steps = o.max_steps; C->a_trace_cap = o.trace_cap; C->a_trace = trace; C->a_rid = rid; C->a_n = n;
 
     init_tconst(M, tb, S, T, lane);
 
@@ -621,7 +640,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     C->count1 = 0; C->phase = PH_F0; C->callSetup = 0; C->jbad = 0; C->jcur_nls = 0; C->hnewOK = 0; C->newj = 0;
     C->p_last = 0.0;
 
+#if BR_PHASE_CLOCKS
     unsigned long long cyc_rhs = 0, cyc_jac = 0, cyc_lu = 0, cyc_sol = 0;
+#define BR_CLK(v) const unsigned long long v = clock64()
+#define BR_ACC(acc, v) acc += clock64() - v
+#else
+#define BR_CLK(v)
+#define BR_ACC(acc, v)
+#endif
     const unsigned long long cyc0 = wall_clock64();
     int perm = lane;
     double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
@@ -629,44 +655,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
         const double y = V[V_Y * WAVE + lane];
         double f;
         {
-            const unsigned long long c0 = clock64();
-#ifndef BR_XNORHS
+            BR_CLK(c0);
             f = rhs(M, tb, S, T, Asv, Asv_th, y, lane, p_last);
-#else
-            f = y;
-#endif
-            cyc_rhs += clock64() - c0;
+            BR_ACC(cyc_rhs, c0);
         }
         double b = 0.0;
-        int act_code = ctl_post_rhs(C, V, lane, f, a, &b);
+        int act_code = ctl_post_rhs(C, V, lane, f, &b);
         if (act_code == A_RHS) continue;
         if (act_code == A_DONE) break;
         int lu_fail = 0;
         if (act_code == A_SETUP) {
             if (ui(C->newj)) {
-                const unsigned long long c0 = clock64();
-#ifndef BR_XNOJAC
+                BR_CLK(c0);
                 jacobian(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
-#endif
-                cyc_jac += clock64() - c0;
+                BR_ACC(cyc_jac, c0);
             }
-            const unsigned long long c1 = clock64();
+            BR_CLK(c1);
             int pstep = 0;
-#ifndef BR_XNOLU
             lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, pstep);
-#endif
             perm = pivot_perm(pstep, lane, n);
-            cyc_lu += clock64() - c1;
+            BR_ACC(cyc_lu, c1);
         }
         double delta = 0.0;
         if (!lu_fail) {
-            const unsigned long long c0 = clock64();
-#ifndef BR_XNOSOLVE
+            BR_CLK(c0);
             delta = lu_solve<NMAX>(LUsave, n, lane, perm, b);
-#endif
-            cyc_sol += clock64() - c0;
+            BR_ACC(cyc_sol, c0);
         }
-        act_code = ctl_post_solve(C, V, lane, delta, lu_fail, a);
+        act_code = ctl_post_solve(C, V, lane, delta, lu_fail);
         if (act_code == A_DONE) break;
     }
     const int status = ui(C->status);
@@ -677,8 +693,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
         st[0] = (double)ui(C->nst); st[1] = (double)ui(C->nfe); st[2] = (double)ui(C->nje);
         st[3] = (double)ui(C->nsetups); st[4] = (double)ui(C->nni); st[5] = (double)ui(C->ncfn);
         st[6] = (double)ui(C->netf); st[7] = (double)status;
-        st[8] = (double)(wall_clock64() - cyc0); st[9] = (double)cyc_rhs; st[10] = (double)cyc_jac;
-        st[11] = (double)cyc_lu; st[12] = (double)cyc_sol; st[13] = ud(C->tn);
+        st[8] = (double)(wall_clock64() - cyc0);
+#if BR_PHASE_CLOCKS
+        st[9] = (double)cyc_rhs; st[10] = (double)cyc_jac; st[11] = (double)cyc_lu; st[12] = (double)cyc_sol;
+#else
+        st[9] = st[10] = st[11] = st[12] = 0.0;
+#endif
+        st[13] = ud(C->tn);
     }
 }
 

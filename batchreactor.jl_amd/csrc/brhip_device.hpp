@@ -49,6 +49,20 @@ struct DevMech {
     const int* col_rx;            // combined reaction index (gas r, surface nrg+r)
 };
 
+// The kernels' first argument is the DevMech (kernarg offset 0). The hot-path functions re-read
+// its fields at the point of use through a laundered kernarg pointer (scalar loads from the
+// kernarg segment), instead of keeping ~40 SGPRs of mechanism fields live across the whole
+// integrator loop (which forced SGPR spills and serialised the LU / solve broadcasts).
+extern __shared__ __attribute__((aligned(16))) char br_lds[];
+template <class T>
+__device__ __forceinline__ T karg_field(size_t off) {
+    const char* p = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    typedef const __attribute__((address_space(4))) T cT;
+    return *(cT*)(p + off);
+}
+#define MF(f) (::brhip::karg_field<decltype(::brhip::DevMech::f)>(offsetof(::brhip::DevMech, f)))
+
 // RX record: w0 reactant species (4 x 8 bit; pad = SP_ONE, a slot holding 1.0, so the
 // concentration products need no branches), w1 product species, w2 info (third-body
 // efficiency set in bits 22..31), w3 pad, w4..w6 net-stoichiometry scatter list, w7 pad
@@ -81,13 +95,14 @@ struct Tab {   // views of the staged table image
 };
 __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
     Tab t;
+    base = br_lds;
     t.molwt = reinterpret_cast<const double*>(base);
     t.sigma = t.molwt + 64;
     t.rx = reinterpret_cast<const uint32_t*>(base + IMG_RX_OFF);
-    t.sx = reinterpret_cast<const uint32_t*>(base + M.sx_off);
-    t.sxe = reinterpret_cast<const double*>(base + M.sxe_off);
-    t.tbe = base + M.tbe_off;
-    t.tbs = reinterpret_cast<const uint32_t*>(base + M.tbs_off);
+    t.sx = reinterpret_cast<const uint32_t*>(base + MF(sx_off));
+    t.sxe = reinterpret_cast<const double*>(base + MF(sxe_off));
+    t.tbe = base + MF(tbe_off);
+    t.tbs = reinterpret_cast<const uint32_t*>(base + MF(tbs_off));
     return t;
 }
 
@@ -180,12 +195,12 @@ __host__ __device__ inline int skd_off_bytes(int nrg, int nfo) { return fod_off_
 __host__ __device__ inline int rblock_bytes(int nrg, int nfo, int nrs) {
     return SP_BYTES + skd_off_bytes(nrg, nfo) + 16 * nrs;
 }
-__device__ __forceinline__ RView rview(char* spbase, const DevMech& M) {
+__device__ __forceinline__ RView rview(char* spbase, const DevMech& /*M*/) {
     RView r;
     r.sp = reinterpret_cast<double*>(spbase);
     r.rxd = reinterpret_cast<double*>(spbase + SP_BYTES);
-    r.fod = reinterpret_cast<double*>(spbase + SP_BYTES + M.fod_off);
-    r.skd = reinterpret_cast<double*>(spbase + SP_BYTES + M.skd_off);
+    r.fod = reinterpret_cast<double*>(spbase + SP_BYTES + MF(fod_off));
+    r.skd = reinterpret_cast<double*>(spbase + SP_BYTES + MF(skd_off));
     return r;
 }
 
@@ -209,8 +224,8 @@ __device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, u
 // stage the table image (all threads of the workgroup), then barrier
 __device__ __forceinline__ void stage_tables(const DevMech& M, char* dst) {
     uint4* d = reinterpret_cast<uint4*>(dst);
-    const int nv = M.img_bytes / 16;
-    for (int i = threadIdx.x; i < nv; i += blockDim.x) d[i] = M.img[i];
+    const int nv = MF(img_bytes) / 16;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) d[i] = MF(img)[i];
     __syncthreads();
 }
 
@@ -220,8 +235,8 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
     double* grt = R.sp + SP_ACCW;
     if (lane == 0) R.sp[SP_ONE] = 1.0;
 #pragma unroll 1
-    for (int k = lane; k < M.ng; k += WAVE) {
-        const double* c = M.nasa + 15 * k;
+    for (int k = lane; k < MF(ng); k += WAVE) {
+        const double* c = MF(nasa) + 15 * k;
         const double* a = (T < c[0]) ? c + 8 : c + 1;
         const double h = a[0] + a[1] * T / 2 + a[2] * T * T / 3 + a[3] * T * T * T / 4 + a[4] * T * T * T * T / 5 + a[5] / T;
         const double s = a[0] * lT + a[1] * T + a[2] * T * T / 2 + a[3] * T * T * T / 3 + a[4] * T * T * T * T / 4 + a[6];
@@ -230,10 +245,10 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
     wave_sync();
     const double RT = R_GAS * T;
 #pragma unroll 1
-    for (int r = lane; r < M.nrg; r += WAVE) {
+    for (int r = lane; r < MF(nrg); r += WAVE) {
         const uint32_t* rec = tb.rx + RX_WORDS * r;
         const uint32_t info = rec[2];
-        const double* gp = M.g_par + 4 * r;
+        const double* gp = MF(g_par) + 4 * r;
         const double kf = gp[0] * exp(gp[1] * lT - gp[2] / T);
         double kr = 0.0;
         if (gi_rev(info)) {
@@ -241,7 +256,7 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
             const int nf = gi_nf(info), nr = gi_nr(info);
             for (int e = 0; e < 4; ++e) if (e < nr) dg += grt[sp8(rec[1], e)];
             for (int e = 0; e < 4; ++e) if (e < nf) dg -= grt[sp8(rec[0], e)];
-            double Kc = exp(-dg) * pow(M.p_std / RT, (double)M.g_dnu[r]);
+            double Kc = exp(-dg) * pow(MF(p_std) / RT, (double)MF(g_dnu)[r]);
             Kc *= gp[3];
             kr = kf / Kc;
         }
@@ -249,7 +264,7 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
         R.rxd[2 * r + 1] = kr;
         if (gi_tb(info) == 2) {
             const int fi = gi_foidx(info);
-            const double* fp = M.fo_par + 8 * fi;
+            const double* fp = MF(fo_par) + 8 * fi;
             double* fo = R.fod + 4 * fi;
             fo[0] = fp[0] * exp(fp[1] * lT - fp[2] / T);
             double fcv = 1.0;
@@ -264,9 +279,9 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
         }
     }
 #pragma unroll 1
-    for (int r = lane; r < M.nrs; r += WAVE) {
+    for (int r = lane; r < MF(nrs); r += WAVE) {
         const uint32_t info = tb.sx[SX_WORDS * r + 4];
-        const double* sp = M.s_par + 4 * r;
+        const double* sp = MF(s_par) + 4 * r;
         double k;
         if (si_stick(info)) k = sp[0] * sqrt(RT / (2 * M_PI * sp[3]));
         else k = sp[0] * pow(T, sp[1]) * exp(-sp[2] / RT);
@@ -302,10 +317,11 @@ __device__ __forceinline__ void falloff(const double* fo, bool troe, double kinf
 
 // third-body concentrations of the efficiency sets: mc[s] = Ctot + sum (eff-1) c over the set's
 // list (one lane per set; the list entries are read 2 at a time so the loads overlap)
-__device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb, double* sp, double Ctot, int lane) {
+__device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb_, double* sp, double Ctot, int lane) {
+    const Tab tb = tab_view(br_lds, M);
     const double* conc = sp + SP_CONC;
 #pragma unroll 1
-    for (int t = lane; t < M.nset; t += WAVE) {
+    for (int t = lane; t < MF(nset); t += WAVE) {
         const uint32_t w = tb.tbs[t];
         const int b = w & 0xFFFFF, e = b + (int)(w >> 20);
         double s0 = Ctot, s1 = 0.0;
@@ -328,23 +344,25 @@ __device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb,
 
 // rates of progress, accumulated straight into the per-species production sums:
 // accw[k] += nu_kr q_r (gas reactions), accs[k] += nu_kr q_r (surface reactions)
-__device__ __forceinline__ void production(const DevMech& M, const Tab& tb, const RView& R, double RT, int lane) {
-    const bool xm = (M.conv & 2) != 0;
+__device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, const RView& R_, double RT, int lane) {
+    const Tab tb = tab_view(br_lds, M);
+    const RView R = rview((char*)R_.sp, M);
+    const bool xm = (MF(conv) & 2) != 0;
     const double* conc = R.sp + SP_CONC;
     double* accw = R.sp + SP_ACCW;
     double* accs = R.sp + SP_ACCS;
 #pragma unroll 1
-    for (int r = lane; r < M.nrg; r += WAVE) {
+    for (int r = lane; r < MF(nrg); r += WAVE) {
         const uint4 ra = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
         const uint4 rb = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
         const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
         const uint32_t info = ra.z;
         const int tbk = gi_tb(info);
         // branch-free mass-action products: unused slots point at conc[SP_ONE] = 1; mechanisms
-        // with at most 3 reactants / products per reaction (M.nu4 == 0, GRI) skip the 4th slot
+        // with at most 3 reactants / products per reaction (MF(nu4) == 0, GRI) skip the 4th slot
         double Pf = (conc[sp8(ra.x, 0)] * conc[sp8(ra.x, 1)]) * conc[sp8(ra.x, 2)];
         double Pb = (conc[sp8(ra.y, 0)] * conc[sp8(ra.y, 1)]) * conc[sp8(ra.y, 2)];
-        if (M.nu4) { Pf *= conc[sp8(ra.x, 3)]; Pb *= conc[sp8(ra.y, 3)]; }
+        if (MF(nu4)) { Pf *= conc[sp8(ra.x, 3)]; Pb *= conc[sp8(ra.y, 3)]; }
         double D = k.x * Pf - k.y * Pb;
         if (tbk) {
             const double Mc = R.sp[SP_MC + gi_tbidx(info)];
@@ -359,7 +377,7 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb, cons
         scatter(accw, rb.x, rb.y, rb.z, D);
     }
 #pragma unroll 1
-    for (int r = lane; r < M.nrs; r += WAVE) {
+    for (int r = lane; r < MF(nrs); r += WAVE) {
         const uint32_t* rec = tb.sx + SX_WORDS * r;
         const int nc = si_ncov(rec[4]);
         const double* xe = tb.sxe + SXE_DOUBLES * r;
@@ -380,10 +398,12 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb, cons
 
 // residual! (src/BatchReactor.jl:312-376) for component `lane`; returns du_lane and writes the
 // diagnosed pressure to *p_out (save_data semantics).
-__device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RView& R, double T, double Asv,
+__device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb_, const RView& R_, double T, double Asv,
                                       double Asv_th, double u, int lane, double* p_out) {
-    const bool gas = lane < M.ng;
-    const bool act = lane < M.n;
+    const Tab tb = tab_view(br_lds, M);
+    const RView R = rview((char*)R_.sp, M);
+    const bool gas = lane < MF(ng);
+    const bool act = lane < MF(n);
     const double Mk = tb.molwt[lane];
     // Y = u/rho, x = (Y/M)/sum(Y/M), p = rho R T / Mbar (:326-338 / :349-353) give the gas
     // concentrations c_k = p x_k / (R T) = u_k / M_k exactly; p = R T sum_k c_k
@@ -391,7 +411,7 @@ __device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RVi
     if (act) { R.sp[SP_CONC + lane] = c; R.sp[SP_ACCW + lane] = 0.0; R.sp[SP_ACCS + lane] = 0.0; }
     const double Ctot = wave_sum(gas ? c : 0.0);
     const double p = R_GAS * T * Ctot;
-    if (M.nset) {
+    if (MF(nset)) {
         wave_sync();
         third_body_sets(M, tb, R.sp, Ctot, lane);
     }
@@ -404,7 +424,7 @@ __device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RVi
     if (lane == 0) *p_out = p;
     if (gas) return (s * Asv + w) * Mk;                          // :345, :363-370
     if (!act) return 0.0;
-    return s * Asv_th * tb.sigma[lane] / M.G;                   // :367 / :370
+    return s * Asv_th * tb.sigma[lane] / MF(G);                   // :367 / :370
 }
 
 // analytic Jacobian d(du)/du, written column by column to the per-reactor workspace
@@ -415,14 +435,16 @@ __device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb, const RVi
 __device__ __forceinline__ double ld_l2(const BR_GLOBAL double* p) {
     return __hip_atomic_load((const double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const RView& R, double T, double Asv,
+__device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const RView& R_, double T, double Asv,
                                          double Asv_th, double u, int lane, double* Jsave_, double* jscr_) {
     BR_GLOBAL double* Jsave = launder(Jsave_);
     BR_GLOBAL double* jscr = launder(jscr_);
-    const bool gas = lane < M.ng;
-    const bool act = lane < M.n;
+    const Tab tb = tab_view(br_lds, M);
+    const RView R = rview((char*)R_.sp, M);
+    const bool gas = lane < MF(ng);
+    const bool act = lane < MF(n);
     const double RT = R_GAS * T;
-    const bool xm = (M.conv & 2) != 0;
+    const bool xm = (MF(conv) & 2) != 0;
     const double Mk = tb.molwt[lane];
     double* conc = R.sp + SP_CONC;
     double* accw = R.sp + SP_ACCW;
@@ -431,12 +453,12 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
     if (act) conc[lane] = c;
     const double Ctot = wave_sum(gas ? c : 0.0);
     wave_sync();
-    if (M.nset) {
+    if (MF(nset)) {
         third_body_sets(M, tb, R.sp, Ctot, lane);
         wave_sync();
     }
 #pragma unroll 1
-    for (int r = lane; r < M.nrg; r += WAVE) {                   // per-reaction multipliers
+    for (int r = lane; r < MF(nrg); r += WAVE) {                   // per-reaction multipliers
         const uint32_t* rec = tb.rx + RX_WORDS * r;
         const uint32_t info = rec[2];
         const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
@@ -460,7 +482,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
         jscr[2 * r + 1] = D * coefM;
     }
 #pragma unroll 1
-    for (int r = lane; r < M.nrs; r += WAVE) {
+    for (int r = lane; r < MF(nrs); r += WAVE) {
         const uint32_t* rec = tb.sx + SX_WORDS * r;
         const int nc = si_ncov(rec[4]);
         double k = R.skd[2 * r];
@@ -474,14 +496,14 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
     __builtin_amdgcn_s_waitcnt(0);   // scratch stores complete before other lanes read them
     wave_sync();
 #pragma unroll 1
-    for (int j = 0; j < M.n; ++j) {
+    for (int j = 0; j < MF(n); ++j) {
         if (act) { accw[lane] = 0.0; accs[lane] = 0.0; }
         wave_sync();
-        const int cb = M.col_ptr[j], ce = M.col_ptr[j + 1];
+        const int cb = MF(col_ptr)[j], ce = MF(col_ptr)[j + 1];
 #pragma unroll 1
         for (int i = cb + lane; i < ce; i += WAVE) {
-            const int rr = M.col_rx[i];
-            if (rr < M.nrg) {
+            const int rr = MF(col_rx)[i];
+            if (rr < MF(nrg)) {
                 const int r = rr;
                 const uint32_t* rec = tb.rx + RX_WORDS * r;
                 const uint32_t info = rec[2];
@@ -502,10 +524,10 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
                     for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= conc[sp8(rec[1], e2)];
                     d -= pre * pr;
                 }
-                if (tbk && j < M.ng) d += ld_l2(jscr + 2 * r + 1) * M.tb_eff[gi_tbidx(info) * M.n + j];
+                if (tbk && j < MF(ng)) d += ld_l2(jscr + 2 * r + 1) * MF(tb_eff)[gi_tbidx(info) * MF(n) + j];
                 scatter(accw, rec[4], rec[5], rec[6], d);
             } else {
-                const int r = rr - M.nrg;
+                const int r = rr - MF(nrg);
                 const uint32_t* rec = tb.sx + SX_WORDS * r;
                 const uint32_t info = rec[4];
                 const int nf = si_nf(info), nc = si_ncov(info);
@@ -519,9 +541,9 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
                     cv[e] = 1.0; dc[e] = 0.0;
                     if (e < nf) {
                         const int s = sp[e];
-                        if (s < M.ng) { cv[e] = conc[s]; dc[e] = 1.0 / tb.molwt[s]; }
+                        if (s < MF(ng)) { cv[e] = conc[s]; dc[e] = 1.0 / tb.molwt[s]; }
                         else if (stick) { cv[e] = conc[s]; dc[e] = 1.0; }
-                        else { cv[e] = conc[s] * M.G / tb.sigma[s]; dc[e] = M.G / tb.sigma[s]; }
+                        else { cv[e] = conc[s] * MF(G) / tb.sigma[s]; dc[e] = MF(G) / tb.sigma[s]; }
                     }
                 }
                 double d = 0.0;
@@ -547,8 +569,8 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb, const 
         const double w = act ? accw[lane] : 0.0;
         const double s = act ? accs[lane] : 0.0;
         double v;
-        if (gas) v = (j < M.ng ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * s;
-        else v = Asv_th * tb.sigma[lane] / M.G * s;
+        if (gas) v = (j < MF(ng) ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * s;
+        else v = Asv_th * tb.sigma[lane] / MF(G) * s;
         Jsave[j * WAVE + lane] = act ? v : 0.0;
         wave_sync();
     }

@@ -8,6 +8,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# per-phase shader clocks are compiled only into the diagnostic build
+os.environ.setdefault("BRHIP_LIB", os.path.join(ROOT, "batchreactor.jl_amd", "libbrhip_diag.so"))
 import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
