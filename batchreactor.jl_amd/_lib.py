@@ -30,7 +30,7 @@ class Opts(C.Structure):
                 ("hmax", C.c_double), ("trace_cap", C.c_int), ("unstable_factor", C.c_double)]
 
 
-NSTAT = 14
+NSTAT = 16
 
 
 EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info",

@@ -77,7 +77,7 @@ __host__ __device__ inline size_t reactor_bytes(const DevMech& M) {
 }
 __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return M.img_bytes + rpb * reactor_bytes(M); }
 // per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn)
-__host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(2 * nmax + 1) * WAVE; }   // Lc, Uc, D
+__host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * WAVE; }   // M, D
 __host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
     return (size_t)nmax * WAVE + lu_ws_doubles(nmax) + (((size_t)2 * nrg + 63) / 64) * 64;
 }
@@ -641,7 +641,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     C->p_last = 0.0;
 
 #if BR_PHASE_CLOCKS
-    unsigned long long cyc_rhs = 0, cyc_jac = 0, cyc_lu = 0, cyc_sol = 0;
+    unsigned long long cyc_rhs = 0, cyc_jac = 0, cyc_lu = 0, cyc_sol = 0, cyc_ctl = 0;
+    const unsigned long long clk0 = clock64();
 #define BR_CLK(v) const unsigned long long v = clock64()
 #define BR_ACC(acc, v) acc += clock64() - v
 #else
@@ -660,7 +661,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
             BR_ACC(cyc_rhs, c0);
         }
         double b = 0.0;
+        BR_CLK(c2);
         int act_code = ctl_post_rhs(C, V, lane, f, &b);
+        BR_ACC(cyc_ctl, c2);
         if (act_code == A_RHS) continue;
         if (act_code == A_DONE) break;
         int lu_fail = 0;
@@ -671,9 +674,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            int pstep = 0;
-            lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, pstep);
-            perm = pivot_perm(pstep, lane, n);
+            lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
         }
         double delta = 0.0;
@@ -682,7 +683,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
             delta = lu_solve<NMAX>(LUsave, n, lane, perm, b);
             BR_ACC(cyc_sol, c0);
         }
+        BR_CLK(c3);
         act_code = ctl_post_solve(C, V, lane, delta, lu_fail);
+        BR_ACC(cyc_ctl, c3);
         if (act_code == A_DONE) break;
     }
     const int status = ui(C->status);
@@ -696,8 +699,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
         st[8] = (double)(wall_clock64() - cyc0);
 #if BR_PHASE_CLOCKS
         st[9] = (double)cyc_rhs; st[10] = (double)cyc_jac; st[11] = (double)cyc_lu; st[12] = (double)cyc_sol;
+        st[14] = (double)cyc_ctl; st[15] = (double)(clock64() - clk0);
 #else
-        st[9] = st[10] = st[11] = st[12] = 0.0;
+        st[9] = st[10] = st[11] = st[12] = st[14] = st[15] = 0.0;
 #endif
         st[13] = ud(C->tn);
     }
@@ -1279,9 +1283,8 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
-    int pstep = 0;
-    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, pstep);
-    const int perm = pivot_perm(pstep, lane, n);
+    int perm = lane;
+    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0);

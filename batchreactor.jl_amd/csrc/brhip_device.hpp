@@ -594,15 +594,19 @@ __device__ __forceinline__ double wave_max_pos(double v) {   // v >= 0 or -1 on 
     v = fmax(v, dppd<0x140>(v));
     return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
 }
-struct LUWs {   // factor workspace (global), columns of 64 lanes
-    BR_GLOBAL double* Lc;
-    BR_GLOBAL double* Uc;
+// Factor workspace (global, per reactor): ONE combined factor matrix, column-major, 64 rows
+// per column, rows in pivot-step order after lu_factor returns: column k holds L[s][k] on rows
+// s > k, U'[s][k] = (D^-1 U)[s][k] on rows s < k and 0 on s = k; then D^-1 in step order.
+// The forward sweep reads only rows below the diagonal and the backward sweep only rows above
+// it (exec-masked loads skip whole 128-B lines), so a solve moves ~n^2 doubles instead of 2*n*64.
+struct LUWs {
+    BR_GLOBAL double* M;
     BR_GLOBAL double* D;
 };
 
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
-// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors, rank-1
-// update of the live columns, shift by one (the loop over k stays rolled).
+// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane =
+// original row), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
 template <int W>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
                                             double& dinv, int& fail, const LUWs& F) {
@@ -619,10 +623,9 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
         const double rinv = 1.0 / piv;
         const bool isp = (lane == p);
         const bool rem = (pstep < 0) && !isp;
-        if (isp) { pstep = k; dinv = rinv; }
         const double l = rem ? a[0] * rinv : 0.0;
-        F.Lc[k * WAVE + lane] = l;
-        F.Uc[k * WAVE + lane] = (pstep >= 0 && !isp) ? a[0] * dinv : 0.0;
+        F.M[k * WAVE + lane] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
+        if (isp) { pstep = k; dinv = rinv; }
         const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
 #pragma unroll
         for (int c = 0; c < W; c += CH) {
@@ -638,74 +641,8 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
     }
 }
 
-// LU in two column panels of P = 32 (registers: 2P per lane, not 2n): panel 1 = columns
-// 0..P-1 factored right-looking; panel 2 = columns P..n-1 first receives the P updates of panel
-// 1 (left-looking: multipliers re-read from Lc, pivot-row values broadcast from the panel-2
-// registers of the pivot lane, in step order), then is factored right-looking. The arithmetic
-// is exactly that of the unblocked right-looking LU. Returns 0 or k+1 for a zero pivot.
-template <int NMAX>
-__device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
-                                         int lane, int& pstep_out) {
-    constexpr int P = NMAX < 32 ? NMAX : 32;
-    constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
-    const BR_GLOBAL double* J = launder(J_);
-    BR_GLOBAL double* wsg = launder(ws);
-    const LUWs F{wsg, wsg + NMAX * WAVE, wsg + 2 * NMAX * WAVE};
-    lane = launder_v(lane);
-    int pstep = (lane < n) ? -1 : 1024;
-    double dinv = 0.0;
-    int fail = 0;
-    const int n1 = n < P ? n : P;
-    {
-        double a[P];
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const double jv = (j < n) ? J[j * WAVE + lane] : 0.0;
-            a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
-        }
-        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F);
-    }
-    if (NMAX > P && n > P) {
-        double b[W2];
-#pragma unroll
-        for (int j = 0; j < W2; ++j) {
-            const int col = P + j;
-            const double jv = (col < n) ? J[col * WAVE + lane] : 0.0;
-            b[j] = ((col == lane) ? 1.0 : 0.0) - gamma * jv;
-        }
-        constexpr int CH = 8;
-        double cur[CH], nxt[CH];
-#pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = F.Lc[i * WAVE + lane];
-#pragma unroll 1
-        for (int kb = 0; kb < P; kb += CH) {
-            if (kb + CH < P) {
-#pragma unroll
-                for (int i = 0; i < CH; ++i) nxt[i] = F.Lc[(kb + CH + i) * WAVE + lane];
-            }
-#pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const int k = kb + i;
-                const unsigned long long m = __ballot(pstep == k);
-                const int p = (int)__builtin_ctzll(m);
-#pragma unroll
-                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), cur[i], b[j]);
-            }
-#pragma unroll
-            for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
-        }
-        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F);
-    }
-    const int npad = (n + 7) & ~7;
-#pragma unroll 1
-    for (int k = n; k < npad; ++k) { F.Lc[k * WAVE + lane] = 0.0; F.Uc[k * WAVE + lane] = 0.0; }
-    F.D[lane] = dinv;
-    pstep_out = pstep;
-    return fail;
-}
-
-// row order after factorization: lane i of the solve works on the pivot row of step i, i.e.
-// original row perm[i] (perm = inverse of pstep); lanes >= n map to themselves
+// row order after factorization: lane s works on the pivot row of step s, i.e. original row
+// perm[s] (perm = inverse of pstep); lanes >= n map to themselves
 __device__ __forceinline__ int pivot_perm(int pstep, int lane, int n) {
     const int dst = (lane < n) ? pstep : lane;
     return __builtin_amdgcn_ds_permute(dst * 4, lane);
@@ -717,51 +654,150 @@ __device__ __forceinline__ double lane_pull(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// one triangular sweep over the zero-padded factor columns col[k*64 + perm] in chunks of 8
-// (forward: k ascending, backward: descending): r -= col_k * r[k]. Two register buffers
-// alternate, so each chunk's loads are issued a full chunk ahead of their use and no register
-// rotation (which would force a wait on the prefetch) is needed.
+// LU in two column panels of P = 32 (registers: 2P per lane, not 2n): panel 1 = columns
+// 0..P-1 factored right-looking; panel 2 = columns P..n-1 first receives the P updates of panel
+// 1 (left-looking: multipliers re-read from M, masked to rows not yet pivoted at that step;
+// pivot-row values broadcast from the panel-2 registers of the pivot lane, in step order), then
+// is factored right-looking. The arithmetic is exactly that of the unblocked right-looking LU.
+// Finally the rows of M are permuted into step order in place (gather, then store), and D^-1
+// is stored in step order. Returns 0 or k+1 for a zero pivot; *perm_out = pivot_perm.
+template <int NMAX>
+__device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
+                                         int lane, int& perm_out) {
+    constexpr int P = NMAX < 32 ? NMAX : 32;
+    constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
+    constexpr int CH = 8;
+    const BR_GLOBAL double* J = launder(J_);
+    BR_GLOBAL double* wsg = launder(ws);
+    const LUWs F{wsg, wsg + NMAX * WAVE};
+    lane = launder_v(lane);
+    const bool act = lane < n;
+    int pstep = act ? -1 : 1024;
+    double dinv = 0.0;
+    int fail = 0;
+    const int n1 = n < P ? n : P;
+    {
+        double a[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const double jv = (j < n && act) ? J[j * WAVE + lane] : 0.0;
+            a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
+        }
+        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F);
+    }
+    if (NMAX > P && n > P) {
+        double b[W2];
+#pragma unroll
+        for (int j = 0; j < W2; ++j) {
+            const int col = P + j;
+            const double jv = (col < n && act) ? J[col * WAVE + lane] : 0.0;
+            b[j] = ((col == lane) ? 1.0 : 0.0) - gamma * jv;
+        }
+        double cur[CH], nxt[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) cur[i] = F.M[i * WAVE + lane];
+#pragma unroll 1
+        for (int kb = 0; kb < P; kb += CH) {
+            if (kb + CH < P) {
+#pragma unroll
+                for (int i = 0; i < CH; ++i) nxt[i] = F.M[(kb + CH + i) * WAVE + lane];
+            }
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const int k = kb + i;
+                const unsigned long long m = __ballot(pstep == k);
+                const int p = (int)__builtin_ctzll(m);
+                const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
+#pragma unroll
+                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), l, b[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
+        }
+        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F);
+    }
+    // rows into step order, in place: chunk c is gathered completely before it is stored, and
+    // the gathers of chunk c+1 are in flight while chunk c is stored (columns >= n: zeros)
+    const int perm = pivot_perm(pstep, lane, n);
+    {
+        constexpr int NC = NMAX / CH;
+        double g[2][CH];
+        auto gather = [&](double (&v)[CH], int c) {
+#pragma unroll
+            for (int i = 0; i < CH; ++i) v[i] = F.M[min(c + i, n - 1) * WAVE + perm];
+        };
+        gather(g[0], 0);
+#pragma unroll
+        for (int t = 0; t < NC; ++t) {
+            if (t + 1 < NC) gather(g[(t + 1) & 1], (t + 1) * CH);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * WAVE + lane] = (t * CH + i < n) ? g[t & 1][i] : 0.0;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    F.D[lane] = lane_pull(dinv, perm);
+    perm_out = perm;
+    return fail;
+}
+
+// one triangular sweep over step-ordered factor columns in chunks of 8 (forward: k ascending,
+// rows s > k; backward: k descending, rows s < k): r[s] -= M[s][k] * r[k], for k < n only.
+// Loads are unconditional (so the compiler's vmcnt waits stay exact and the prefetch is real):
+// rows a chunk cannot touch re-read a row it does touch (same 128-B lines, no extra traffic)
+// and columns past n re-read column n-1; the per-column lane masks discard what they feed.
+// Two register buffers alternate: each chunk's loads are issued a full chunk ahead of use.
 template <bool FWD>
-__device__ __forceinline__ void tri_chunk(const double (&v)[8], int c, double& r) {
+__device__ __forceinline__ void tri_chunk(const double (&v)[8], int c, int lo, int n, double& r) {
 #pragma unroll
     for (int ii = 0; ii < 8; ++ii) {
         const int i = FWD ? ii : 7 - ii;
-        r = fma(-v[i], bcast(r, c + i), r);
+        const int k = c + i;
+        const double x = bcast(r, k < n ? k : 0);
+        // forward: lo = lane (lanes >= n: -1); backward: lo = lane, limit min(k, n) with k >= n -> none
+        const bool upd = FWD ? (lo > k) : (lo < ((k < n) ? k : 0));
+        const double t = fma(-v[i], x, r);
+        r = upd ? t : r;
     }
 }
 template <bool FWD>
-__device__ __forceinline__ void tri_load(double (&v)[8], const BR_GLOBAL double* __restrict__ col, int c) {
+__device__ __forceinline__ void tri_load(double (&v)[8], const BR_GLOBAL double* __restrict__ col, int c, int lane,
+                                         int n) {
+    // columns [n, roundup8(n)) are stored as zeros; later chunks are in bounds and masked
+    const int row = FWD ? min(max(lane, c + 1), n - 1) : min(min(lane, c + 7), n - 1);
+    const BR_GLOBAL double* p = col + c * WAVE + row;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = col[(c + i) * WAVE];
+    for (int i = 0; i < 8; ++i) v[i] = p[i * WAVE];
 }
-template <bool FWD>
-__device__ __forceinline__ double tri_sweep(const BR_GLOBAL double* __restrict__ col, int nch, double r) {
-    double A[8], B[8];
-    auto cidx = [&](int t) { return FWD ? t * 8 : (nch - 1 - t) * 8; };
-    tri_load<FWD>(A, col, cidx(0));
-    if (nch > 1) tri_load<FWD>(B, col, cidx(1));
-#pragma unroll 1
-    for (int t = 0; t < nch; t += 2) {
-        tri_chunk<FWD>(A, cidx(t), r);
-        if (t + 2 < nch) tri_load<FWD>(A, col, cidx(t + 2));
-        if (t + 1 < nch) {
-            tri_chunk<FWD>(B, cidx(t + 1), r);
-            if (t + 3 < nch) tri_load<FWD>(B, col, cidx(t + 3));
-        }
+template <bool FWD, int NCH>
+__device__ __forceinline__ double tri_sweep(const BR_GLOBAL double* __restrict__ col, int lane, int n, double r) {
+    double A[2][8];
+    auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
+    const int lo = FWD ? ((lane < n) ? lane : -1) : lane;
+    tri_load<FWD>(A[0], col, cidx(0), lane, n);
+    if (NCH > 1) tri_load<FWD>(A[1], col, cidx(1), lane, n);
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {          // fully unrolled: exact vmcnt waits for the prefetch
+        __builtin_amdgcn_sched_barrier(0);   // loads stay a full chunk ahead of their use
+        tri_chunk<FWD>(A[t & 1], cidx(t), lo, n, r);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < NCH) tri_load<FWD>(A[t & 1], col, cidx(t + 2), lane, n);
     }
     return r;
 }
 
 // solve (I - gamma J) x = b with the factors of lu_factor: L y = P b, y' = D^-1 y, U' x = y'.
-// `perm` from pivot_perm; b and the returned x are in natural component order.
+// `perm` from lu_factor; b and the returned x are in natural component order (the backward
+// sweep leaves unknown s, i.e. column s, on lane s).
 template <int NMAX>
 __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n, int lane, int perm, double b) {
     const BR_GLOBAL double* wsg = launder(ws);
-    const int nch = (n + 7) >> 3;
-    double r = lane_pull(b, perm);                 // P b
-    r = tri_sweep<true>(wsg + perm, nch, r);       // forward, unit lower
-    r *= wsg[2 * NMAX * WAVE + perm];              // D^-1
-    r = tri_sweep<false>(wsg + NMAX * WAVE + perm, nch, r);   // backward, unit upper
+    lane = launder_v(lane);
+    constexpr int NCH = NMAX / 8;
+    double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
+    r = tri_sweep<true, NCH>(wsg, lane, n, r);     // forward, unit lower
+    r *= wsg[NMAX * WAVE + lane];                  // D^-1
+    r = tri_sweep<false, NCH>(wsg, lane, n, r);    // backward, unit upper
     return (lane < n) ? r : 0.0;
 }
 

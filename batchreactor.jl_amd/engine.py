@@ -18,7 +18,7 @@ from . import _lib
 from .mechanism import Mechanism
 
 STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status", "cyc_total", "cyc_rhs",
-               "cyc_jac", "cyc_lu", "cyc_sol", "t_end")
+               "cyc_jac", "cyc_lu", "cyc_sol", "t_end", "cyc_ctl", "cyc_clk")
 
 
 class Engine:

@@ -88,12 +88,14 @@ typedef struct br_opts {
                                  factor * sum_k |u0_k| (0 = default 10, < 0 = never)     */
 } br_opts;
 
-#define BR_NSTAT 14
+#define BR_NSTAT 16
 typedef struct br_stats {     /* per reactor; counters as CVODE's, then device cycles */
     double nsteps, nfe, nje, nsetups, nni, ncfn, netf, status;
     double cyc_total;         /* wall clock ticks (100 MHz) for the whole reactor  */
     double cyc_rhs, cyc_jac, cyc_lu, cyc_sol;  /* shader clocks in each phase      */
     double t_end;             /* time reached                                      */
+    double cyc_ctl;           /* shader clocks in the step controller (diagnostic build) */
+    double cyc_clk;           /* shader clocks for the whole reactor (diagnostic build)  */
 } br_stats;
 
 int         br_version(void);

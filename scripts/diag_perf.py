@@ -35,8 +35,12 @@ for k in ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf"):
     print(f"  {k:8s} mean {v.mean():9.1f} p50 {np.median(v):8.0f} p99 {np.percentile(v, 99):8.0f} max {v.max():8.0f}")
 tot = st["cyc_total"] / 100e6
 print(f"  wave time ms: mean {tot.mean()*1e3:.2f} p50 {np.median(tot)*1e3:.2f} max {tot.max()*1e3:.2f}")
-for ph, cnt in (("rhs", "nfe"), ("jac", "nje"), ("lu", "nsetups"), ("sol", "nni")):
+clk = np.sum(st["cyc_clk"])
+print(f"  shader clocks per reactor {clk/N:.4g} (clock ratio to 100 MHz wall: {clk/np.sum(st['cyc_total']):.1f})")
+for ph, cnt in (("rhs", "nfe"), ("jac", "nje"), ("lu", "nsetups"), ("sol", "nni"), ("ctl", "nfe")):
     c = st["cyc_" + ph]
-    print(f"  {ph:4s} cycles/call {np.sum(c)/max(np.sum(st[cnt]),1):10.0f}  share of clock {np.sum(c)/np.sum(st['cyc_rhs']+st['cyc_jac']+st['cyc_lu']+st['cyc_sol']):.3f}")
+    print(f"  {ph:4s} cycles/call {np.sum(c)/max(np.sum(st[cnt]),1):10.0f}  share of clock {np.sum(c)/clk:.3f}")
+rest = clk - sum(np.sum(st["cyc_" + ph]) for ph in ("rhs", "jac", "lu", "sol", "ctl"))
+print(f"  rest (init, loop glue): share {rest/clk:.3f}")
 i = int(np.argmax(st["nsteps"]))
 print("slowest reactor", i, "T", T[i], {k: float(st[k][i]) for k in pkg.STAT_FIELDS})
