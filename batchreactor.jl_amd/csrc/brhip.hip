@@ -134,6 +134,11 @@ __device__ __forceinline__ CtlArgs load_args(LCtl* C) {
     return a;
 }
 
+// 1.0 / j for the small integers of the BDF coefficient formulas (exactly the rounded quotient)
+__device__ __forceinline__ double inv_int(int j) {
+    return j == 1 ? 1.0 : j == 2 ? 0.5 : j == 3 ? 1.0 / 3.0 : j == 4 ? 0.25 : j == 5 ? 0.2 : j == 6 ? 1.0 / 6.0 : 1.0 / j;
+}
+
 // cvSet (BDF coefficients l[], tq[], gamma) for the current q, h, tau
 __device__ __forceinline__ void cv_set(LCtl* C) {
     const int q = ui(C->q), qwait = ui(C->qwait), nst = ui(C->nst);
@@ -147,11 +152,11 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
         for (int j = 2; j < q; ++j) {
             hsum += tau[j - 1];
             xi_inv = h / hsum;
-            alpha0 -= 1.0 / j;
+            alpha0 -= inv_int(j);
 #pragma unroll
             for (int i = QMAX; i >= 1; --i) if (i <= j) lv[i] += lv[i - 1] * xi_inv;
         }
-        alpha0 -= 1.0 / q;
+        alpha0 -= inv_int(q);
         xistar_inv = -lv[1] - alpha0;
         hsum += tau[q - 1];
         xi_inv = h / hsum;
@@ -170,14 +175,14 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
     if (qwait == 1) {
         if (q > 1) {
             const double Cc = xistar_inv / lq;
-            const double A3 = alpha0 + 1.0 / q;
+            const double A3 = alpha0 + inv_int(q);
             const double A4 = alpha0_hat + xi_inv;
             const double Cpinv = (1.0 - A4 + A3) / A3;
             C->tq[1] = fabs(Cc * Cpinv);
         } else C->tq[1] = 1.0;
         hsum += tau[q];
         xi_inv = h / hsum;
-        const double A5 = alpha0 - (1.0 / (q + 1));
+        const double A5 = alpha0 - inv_int(q + 1);
         const double A6 = alpha0_hat - xi_inv;
         const double Cppinv = (1.0 - A6 + A5) / A2;
         C->tq[3] = fabs(Cppinv / (xi_inv * (q + 2) * A5));
@@ -244,7 +249,7 @@ __device__ __forceinline__ void cv_adjust_order(LCtl* C, LDbl* V, int lane, int 
             hsum += ud(C->tau[j + 1]);
             const double xi = hsum / hscale;
             prod *= xi;
-            alpha0 -= 1.0 / (j + 1);
+            alpha0 -= inv_int(j + 1);
             alpha1 += 1.0 / xi;
 #pragma unroll
             for (int i = QMAX; i >= 2; --i) if (i <= j + 2) lv[i] = lv[i] * xiold + lv[i - 1];
@@ -404,6 +409,29 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, 
     return A_RHS;
 }
 
+// x^(1/L) for the step-size ratios (L = order + 1 <= 6): hardware fp32 log2/exp2 estimate and
+// two fp64 Newton steps (within a few ulp of pow(x, 1.0/L), which CVODE uses; ~40 instructions
+// instead of ~280 for the generic pow); outside [1e-30, 1e30] the generic pow
+__device__ __forceinline__ double root_int(double x, int L) {
+    if (L == 1) return x;
+    if (L == 2) return sqrt(x);
+    if (!(x >= 1e-30 && x <= 1e30)) return pow(x, 1.0 / L);
+    double y = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf((float)x) / (float)L);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        double p = y;                                  // y^(L-1)
+        for (int k = 2; k < L; ++k) p *= y;
+        y -= (p * y - x) / (L * p);
+    }
+    return y;
+}
+// x^L for the small integer L of cvPrepareNextStep (repeated products; pow in CVODE)
+__device__ __forceinline__ double pow_int(double x, int L) {
+    double p = x;
+    for (int k = 1; k < L; ++k) p *= x;
+    return p;
+}
+
 // Controller, part 2: after the linear solve (delta = this lane's Newton correction) or after
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
@@ -472,7 +500,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
         if (nef == MXNEF) { C->status = BR_ERR_ERRTEST; return A_DONE; }
         C->etamax = 1.0;
         if (nef <= MXNEF1) {
-            double eta = 1.0 / (pow(BIAS2 * dsm, 1.0 / ui(C->L)) + ADDON);
+            double eta = 1.0 / (root_int(BIAS2 * dsm, ui(C->L)) + ADDON);
             eta = fmax(ETAMIN, eta);
             if (nef >= SMALL_NEF) eta = fmin(eta, ETAMXF);
             C->eta = eta;
@@ -515,21 +543,21 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
         qwait = qwait > 2 ? qwait : 2;
     } else {
         const int L = ui(C->L);
-        const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / L) + ADDON);
+        const double etaq = 1.0 / (root_int(BIAS2 * dsm, L) + ADDON);
         if (qwait != 0) { eta = etaq; }
         else {
             qwait = 2;
             double etaqm1 = 0.0, etaqp1 = 0.0;
             if (q > 1) {
                 const double ddn = wrms_l(V[q * WAVE + lane], ewt, lane, n) * ud(C->tq[1]);
-                etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / q) + ADDON);
+                etaqm1 = 1.0 / (root_int(BIAS1 * ddn, q) + ADDON);
             }
             const double saved_tq5 = ud(C->saved_tq5);
             if (q != QMAX && saved_tq5 != 0.0) {
-                const double cquot = (ud(C->tq[5]) / saved_tq5) * pow(h / ud(C->tau[2]), (double)L);
+                const double cquot = (ud(C->tq[5]) / saved_tq5) * pow_int(h / ud(C->tau[2]), L);
                 const double tempv = acor - cquot * V[QMAX * WAVE + lane];
                 const double dup = wrms_l(tempv, ewt, lane, n) * ud(C->tq[3]);
-                etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (L + 1)) + ADDON);
+                etaqp1 = 1.0 / (root_int(BIAS3 * dup, L + 1) + ADDON);
             }
             const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
             if (etam < THRESH) { eta = 1.0; }
