@@ -579,20 +579,32 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
 // ------------------------------------------------------------------------------------
 // LU of A = I - gamma*J, row-per-lane (SUNDIALS denseGETRF semantics: partial pivoting on the
 // first max |a_ik| in row order, multipliers l_ik = a_ik / a_kk, a_ij -= l_ik a_kj), without
-// physical row swaps. The factors are stored for a mask-free solve, per original row (lane):
-//   Lc[k][row] = l_row,k if the row was still unpivoted at step k, else 0;
-//   Uc[k][row] = u_row,k / u_row,row if the row was pivoted before step k, else 0 (unit-diagonal
-//                U' = D^-1 U);  D[row] = 1 / u_row,row.
-// Columns n..roundup8(n)-1 of Lc/Uc are written as zeros, so the solve needs no k < n tests.
-// Pivot search: wave max of |a_k| over the remaining rows (DPP on the two dwords + v_max_f64),
-// then the lowest lane holding that value (ballot + ff1) = the first max in row order.
+// physical row swaps during the factorization (see LUWs for the stored form).
+// Pivot search on the bit patterns of |a_ik| (monotone for non-negative doubles): a 32-bit
+// DPP max over the high words, a second pass over the low words only when the high words tie,
+// then the lowest candidate lane holding the max (ballot + ff1) = the first max in row order.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_max_pos(double v) {   // v >= 0 or -1 on idle lanes
-    v = fmax(v, dppd<0xB1>(v));
-    v = fmax(v, dppd<0x4E>(v));
-    v = fmax(v, dppd<0x141>(v));
-    v = fmax(v, dppd<0x140>(v));
-    return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
+__device__ __forceinline__ unsigned wave_umax(unsigned x) {
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
+    const unsigned r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
+    const unsigned r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+__device__ __forceinline__ int pivot_lane(double v, bool cand) {   // v = |a_ik| on candidate rows
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+    const unsigned hi = cand ? (unsigned)(bits >> 32) : 0u;
+    const unsigned mh = wave_umax(hi);
+    const bool top = cand && hi == mh;
+    unsigned long long m = __ballot(top);
+    if (__builtin_popcountll(m) > 1) {
+        const unsigned lo = top ? (unsigned)bits : 0u;
+        const unsigned ml = wave_umax(lo);
+        m = __ballot(top && lo == ml);
+    }
+    return m ? (int)__builtin_ctzll(m) : 0;
 }
 // Factor workspace (global, per reactor): ONE combined factor matrix, column-major, 64 rows
 // per column, rows in pivot-step order after lu_factor returns: column k holds L[s][k] on rows
@@ -614,10 +626,7 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
     static_assert(W % CH == 0, "W must be a multiple of 8");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
-        const double v = (pstep < 0) ? fabs(a[0]) : -1.0;
-        const double vmax = wave_max_pos(v);
-        const unsigned long long hit = __ballot(pstep < 0 && v == vmax);
-        const int p = hit ? (int)__builtin_ctzll(hit) : 0;
+        const int p = pivot_lane(fabs(a[0]), pstep < 0);
         const double piv = bcast(a[0], p);
         if (piv == 0.0 && !fail) fail = k + 1;
         const double rinv = 1.0 / piv;
