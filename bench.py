@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--n", type=int, default=0, help="reactors per GPU (default: the config's N)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_gri.json"),
+                    help="PMC summary (scripts/pmc_traffic.py) giving HBM bytes per reactor for roofline.traffic")
     args = ap.parse_args()
 
     import torch
@@ -103,6 +105,13 @@ def main():
     kernel_ms = float(np.mean(kms))
     achieved = flops / (kernel_ms * 1e-3) / 1e12
 
+    # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
+    # kernel on this workload (bytes per reactor x reactors in this launch); None if absent
+    traffic = None
+    if args.config == "gri" and os.path.exists(args.traffic):
+        with open(args.traffic) as fh:
+            traffic = json.load(fh)["bytes_per_reactor"] * N
+
     gather_ms = None
     if world > 1:   # the single result gather over RCCL/xGMI (outside the timed region)
         payload = torch.cat([dU, dst], dim=1).contiguous()
@@ -138,7 +147,8 @@ def main():
             "config": {"workload": cfg["name"], "reactors_per_gpu": N, "total_reactors": total,
                        "tf_s": cfg["tf"], "rtol": 1e-6, "atol": 1e-10, "parallelism": f"ensemble dp{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_unit": "B per launch (PMC, profiles/traffic_gri.json)",
                          "kernel": f"k_integrate<{eng.nmax}>", "kernel_ms": kernel_ms,
                          "algorithmic_flop_per_launch": flops},
             "cpu_baseline": cpu,
