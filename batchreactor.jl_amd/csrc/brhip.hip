@@ -68,18 +68,21 @@ struct Ctl {
 };
 constexpr int CTL_BYTES = (sizeof(Ctl) + 15) / 16 * 16;
 enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, acor, ewt, tempv, y
-constexpr int VEC_BYTES = NVEC * WAVE * 8;
+// V[vec * VW + component], VW = 64 * CPL components per vector
+__host__ __device__ inline int vec_bytes(int cpl) { return NVEC * WAVE * cpl * 8; }
 typedef __attribute__((address_space(3))) Ctl LCtl;
 typedef __attribute__((address_space(3))) double LDbl;
 
 __host__ __device__ inline size_t reactor_bytes(const DevMech& M) {
-    return CTL_BYTES + VEC_BYTES + (size_t)M.rblock_bytes;
+    return CTL_BYTES + vec_bytes(M.cpl) + (size_t)M.rblock_bytes;
 }
 __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return M.img_bytes + rpb * reactor_bytes(M); }
-// per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn)
-__host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * WAVE; }   // M, D
+// per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn);
+// matrix columns hold 64 * CPL rows (CPL = 2 for nmax > 64)
+__host__ __device__ inline int col_rows(int nmax) { return nmax > 64 ? 128 : 64; }
+__host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * col_rows(nmax); }   // M, D
 __host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
-    return (size_t)nmax * WAVE + lu_ws_doubles(nmax) + (((size_t)2 * nrg + 63) / 64) * 64;
+    return (size_t)nmax * col_rows(nmax) + lu_ws_doubles(nmax) + (((size_t)2 * nrg + 63) / 64) * 64;
 }
 
 struct WaveCtx {
@@ -88,15 +91,16 @@ struct WaveCtx {
     char* rbase;   // this wave's reactor block
     RView R;
 };
+template <int CPL>
 __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rpb) {
     WaveCtx w;
     w.wave = uni((int)(threadIdx.x >> 6));   // uniform per wave: scalar addressing of its reactor
     w.lane = threadIdx.x & 63;
     w.rid = blockIdx.x * rpb + w.wave;
     stage_tables(M, smem);
-    w.tb = tab_view(smem, M);
+    w.tb = tab_view<CPL>(smem, M);
     w.rbase = smem + M.img_bytes + (size_t)w.wave * reactor_bytes(M);
-    w.R = rview(w.rbase + CTL_BYTES + VEC_BYTES, M);
+    w.R = rview<CPL>(w.rbase + CTL_BYTES + vec_bytes(CPL), M);
     return w;
 }
 
@@ -111,11 +115,20 @@ enum { PH_F0 = 0, PH_HIN = 1, PH_NEWTON = 2, PH_EF1 = 3 };
 // action codes returned by the controller to the hot loop
 enum { A_RHS = 0, A_SOLVE = 1, A_SETUP = 2, A_DONE = 3 };
 
-// wrms norm of a per-lane value with the weights in V[V_EWT]
-__device__ __forceinline__ double wrms_l(double v, double ewt, int lane, int n) {
-    const double t = (lane < n) ? v * ewt : 0.0;
-    return uni(sqrt(wave_sum(t * t) / n));
+// wrms norm of the lane's component values (components lane + 64 s) with weights ewt
+template <int CPL>
+__device__ __forceinline__ double wrms_l(const double (&v)[CPL], const double (&ewt)[CPL], int lane, int n) {
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < CPL; ++s) {
+        const double t = (lane + 64 * s < n) ? v[s] * ewt[s] : 0.0;
+        acc += t * t;
+    }
+    return uni(sqrt(wave_sum(acc) / n));
 }
+// per-component slot loops over the lane's components c = lane + 64 s
+#define FOR_S for (int s = 0; s < CPL; ++s)
+#define CS (lane + 64 * s)
 
 struct CtlArgs {   // per-launch constants the controller needs, read (uniform) from the LDS controller
     double rtol, atol, hmax_inv, ufac;
@@ -197,48 +210,66 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
 }
 
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
+template <int CPL>
 __device__ __forceinline__ void cv_rescale(LCtl* C, LDbl* V, int lane) {
+    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     const double eta = ud(C->eta);
     double f = eta;
-    for (int j = 1; j <= q; ++j) { V[j * WAVE + lane] *= f; f *= eta; }
+    for (int j = 1; j <= q; ++j) {
+#pragma unroll
+        FOR_S V[j * VW + CS] *= f;
+        f *= eta;
+    }
     const double h = ud(C->hscale) * eta;
     C->h = h; C->hscale = h;
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
+template <int CPL>
 __device__ __forceinline__ void cv_predict(LCtl* C, LDbl* V, int lane) {
+    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     double tn = ud(C->tn) + ud(C->h);
     const double tstop = ud(C->tstop);
     if ((tn - tstop) * ud(C->h) > 0) tn = tstop;
     C->tn = tn;
-    double z[QMAX + 1];
 #pragma unroll
-    for (int j = 0; j <= QMAX; ++j) z[j] = V[j * WAVE + lane];
+    FOR_S {
+        double z[QMAX + 1];
 #pragma unroll
-    for (int k = 1; k <= QMAX; ++k)
+        for (int j = 0; j <= QMAX; ++j) z[j] = V[j * VW + CS];
 #pragma unroll
-        for (int j = QMAX; j >= k; --j)
-            if (j <= q && k <= q) z[j - 1] += z[j];
+        for (int k = 1; k <= QMAX; ++k)
 #pragma unroll
-    for (int j = 0; j < QMAX; ++j) V[j * WAVE + lane] = z[j];
+            for (int j = QMAX; j >= k; --j)
+                if (j <= q && k <= q) z[j - 1] += z[j];
+#pragma unroll
+        for (int j = 0; j < QMAX; ++j) V[j * VW + CS] = z[j];
+    }
 }
+template <int CPL>
 __device__ __forceinline__ void cv_restore(LCtl* C, LDbl* V, int lane) {
+    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     C->tn = ud(C->saved_t);
-    double z[QMAX + 1];
 #pragma unroll
-    for (int j = 0; j <= QMAX; ++j) z[j] = V[j * WAVE + lane];
+    FOR_S {
+        double z[QMAX + 1];
 #pragma unroll
-    for (int k = 1; k <= QMAX; ++k)
+        for (int j = 0; j <= QMAX; ++j) z[j] = V[j * VW + CS];
 #pragma unroll
-        for (int j = QMAX; j >= k; --j)
-            if (j <= q && k <= q) z[j - 1] -= z[j];
+        for (int k = 1; k <= QMAX; ++k)
 #pragma unroll
-    for (int j = 0; j < QMAX; ++j) V[j * WAVE + lane] = z[j];
+            for (int j = QMAX; j >= k; --j)
+                if (j <= q && k <= q) z[j - 1] -= z[j];
+#pragma unroll
+        for (int j = 0; j < QMAX; ++j) V[j * VW + CS] = z[j];
+    }
 }
 // cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
+template <int CPL>
 __device__ __forceinline__ void cv_adjust_order(LCtl* C, LDbl* V, int lane, int dq) {
+    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     if (q == 2 && dq != 1) return;
     double lv[QMAX + 1] = {0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
@@ -256,10 +287,13 @@ __device__ __forceinline__ void cv_adjust_order(LCtl* C, LDbl* V, int lane, int 
             xiold = xi;
         }
         const double A1 = (-alpha0 - alpha1) / prod;
-        const double zL = A1 * V[QMAX * WAVE + lane];
 #pragma unroll
-        for (int j = 2; j <= QMAX; ++j) if (j <= q) V[j * WAVE + lane] += lv[j] * zL;
-        V[(q + 1) * WAVE + lane] = zL;
+        FOR_S {
+            const double zL = A1 * V[QMAX * VW + CS];
+#pragma unroll
+            for (int j = 2; j <= QMAX; ++j) if (j <= q) V[j * VW + CS] += lv[j] * zL;
+            V[(q + 1) * VW + CS] = zL;
+        }
     } else {
         double hsum = 0.0;
         for (int j = 1; j <= q - 2; ++j) {
@@ -268,63 +302,87 @@ __device__ __forceinline__ void cv_adjust_order(LCtl* C, LDbl* V, int lane, int 
 #pragma unroll
             for (int i = QMAX; i >= 2; --i) if (i <= j + 2) lv[i] = lv[i] * xi + lv[i - 1];
         }
-        const double zq = V[q * WAVE + lane];
 #pragma unroll
-        for (int j = 2; j < QMAX; ++j) if (j < q) V[j * WAVE + lane] -= lv[j] * zq;
+        FOR_S {
+            const double zq = V[q * VW + CS];
+#pragma unroll
+            for (int j = 2; j < QMAX; ++j) if (j < q) V[j * VW + CS] -= lv[j] * zq;
+        }
     }
 }
-__device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, int step, double t, double v) {
+// trace row of an accepted step (save_data, src/BatchReactor.jl:383-402): t, h, q, the pressure
+// of the last RHS evaluation, the accepted state u_n, the state y of the last RHS evaluation
+template <int CPL>
+__device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, int step, double t,
+                                          const double (&v)[CPL], const double (&y)[CPL]) {
     if (a.trace && step <= a.trace_cap) {
-        double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + step) * (a.n + 4);
+        double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + step) * (2 * a.n + 4);
         if (lane == 0) { row[0] = t; row[1] = ud(C->h); row[2] = (double)ui(C->q); row[3] = ud(C->p_last); }
-        if (lane < a.n) row[4 + lane] = v;
+#pragma unroll
+        FOR_S if (CS < a.n) { row[4 + CS] = v[s]; row[4 + a.n + CS] = y[s]; }
     }
 }
 // one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
+template <int CPL>
 __device__ __forceinline__ void begin_attempt(LCtl* C, LDbl* V, int lane, int nflag) {
-    cv_predict(C, V, lane);
+    constexpr int VW = 64 * CPL;
+    cv_predict<CPL>(C, V, lane);
     cv_set(C);
     const int nst = ui(C->nst);
     C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
     C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
                    (nst >= ui(C->nstlp) + MSBP) || (fabs(ud(C->gamrat) - 1.0) > DGMAX);
-    V[V_ACOR * WAVE + lane] = 0.0;
+#pragma unroll
+    FOR_S V[V_ACOR * VW + CS] = 0.0;
     C->tol = ud(C->tq[4]);
     C->jbad = 0;
     C->jcur_nls = 0;
     C->m_it = 0;
-    V[V_Y * WAVE + lane] = V[lane];   // y = z0
+#pragma unroll
+    FOR_S V[V_Y * VW + CS] = V[CS];   // y = z0
 }
+template <int CPL>
 __device__ __forceinline__ void begin_step(LCtl* C, LDbl* V, int lane, const CtlArgs& a) {
-    const double z0 = V[lane];
-    V[V_EWT * WAVE + lane] = (lane < a.n) ? 1.0 / (a.rtol * fabs(z0) + a.atol) : 1.0;
+    constexpr int VW = 64 * CPL;
+#pragma unroll
+    FOR_S {
+        const double z0 = V[CS];
+        V[V_EWT * VW + CS] = (CS < a.n) ? 1.0 / (a.rtol * fabs(z0) + a.atol) : 1.0;
+    }
     C->saved_t = ud(C->tn);
     C->ncf = 0; C->nef = 0;
     if ((ui(C->nst) > 0) && (ud(C->hprime) != ud(C->h))) {
         const int qp = ui(C->qprime), q = ui(C->q);
         if (qp != q) {
-            cv_adjust_order(C, V, lane, qp - q);
+            cv_adjust_order<CPL>(C, V, lane, qp - q);
             C->q = qp; C->L = qp + 1; C->qwait = qp + 1;
         }
-        cv_rescale(C, V, lane);
+        cv_rescale<CPL>(C, V, lane);
     }
-    begin_attempt(C, V, lane, FIRST_CALL);
+    begin_attempt<CPL>(C, V, lane, FIRST_CALL);
 }
 
 // Controller, part 1: after the RHS value f = F(y) of this lane is known.
 // Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
-__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, double* rhs_out) {
+template <int CPL>
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
+    constexpr int VW = 64 * CPL;
     const CtlArgs a = load_args(C);
     const int n = a.n;
-    const bool act = lane < n;
     C->nfe = ui(C->nfe) + 1;
     const int phase = ui(C->phase);
-    const double z0 = V[lane];
+    double z0[CPL];
+#pragma unroll
+    FOR_S z0[s] = V[CS];
     if (phase == PH_NEWTON) {
-        const double acor = V[V_ACOR * WAVE + lane];
-        const double delta = (ud(C->rl1) * V[WAVE + lane] + acor) - ud(C->gamma) * f;   // cvNlsResidual
-        *rhs_out = -delta;
+        const double rl1 = ud(C->rl1), gamma = ud(C->gamma);
+#pragma unroll
+        FOR_S {
+            const double acor = V[V_ACOR * VW + CS];
+            const double delta = (rl1 * V[VW + CS] + acor) - gamma * f[s];   // cvNlsResidual
+            rhs_out[s] = -delta;
+        }
         if (ui(C->m_it) == 0 && ui(C->callSetup)) {          // cvLsSetup decision
             const int nst = ui(C->nst);
             const double dgamma = fabs(ud(C->gamma) / ud(C->gammap) - 1.0);
@@ -342,20 +400,30 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, 
     }
     double h = 0.0;
     if (phase == PH_EF1) {   // restart at order 1 after repeated error-test failures
-        V[WAVE + lane] = ud(C->h) * f;
-        begin_attempt(C, V, lane, PREV_ERR_FAIL);
+        const double hh = ud(C->h);
+#pragma unroll
+        FOR_S V[VW + CS] = hh * f[s];
+        begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
         C->phase = PH_NEWTON;
         return A_RHS;
     }
-    const double z1in = (phase == PH_F0) ? f : V[WAVE + lane];
-    const double ewt = V[V_EWT * WAVE + lane];
+    double z1in[CPL], ewt[CPL];
+#pragma unroll
+    FOR_S {
+        z1in[s] = (phase == PH_F0) ? f[s] : V[VW + CS];
+        ewt[s] = V[V_EWT * VW + CS];
+    }
     if (phase == PH_F0) {
-        V[WAVE + lane] = f;
         const double tn = ud(C->tn), tstop = ud(C->tstop);
         const double tdist = fabs(tstop - tn);
         const double tround = UROUND * fmax(fabs(tn), fabs(tstop));
         const double hlb = HLB_FACTOR * tround;
-        const double ratio = act ? fabs(f) / (HUB_FACTOR * fabs(z0) + 1.0 / ewt) : 0.0;
+        double ratio = 0.0;
+#pragma unroll
+        FOR_S {
+            V[VW + CS] = f[s];
+            if (CS < n) ratio = fmax(ratio, fabs(f[s]) / (HUB_FACTOR * fabs(z0[s]) + 1.0 / ewt[s]));
+        }
         const double hub_inv = uni(wave_max(ratio));
         double hub = HUB_FACTOR * tdist;
         if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
@@ -365,15 +433,18 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, 
             h = hg;
         } else {
             C->count1 = 1; C->hnewOK = 0; C->hnew = hg;
-            V[V_Y * WAVE + lane] = hg * f + z0;
+#pragma unroll
+            FOR_S V[V_Y * VW + CS] = hg * f[s] + z0[s];
             C->phase = PH_HIN;
             return A_RHS;
         }
     } else {                 // PH_HIN (cvYddNorm + the cvHin iteration)
         double hg = ud(C->hg);
         const double hub = ud(C->hub), hlb = ud(C->hlb);
-        const double tempv = (f - z1in) * (1.0 / hg);
-        const double yddnrm = wrms_l(tempv, ewt, lane, n);
+        double tempv[CPL];
+#pragma unroll
+        FOR_S tempv[s] = (f[s] - z1in[s]) * (1.0 / hg);
+        const double yddnrm = wrms_l<CPL>(tempv, ewt, lane, n);
         const int count1 = ui(C->count1);
         double hnew;
         if (ui(C->hnewOK) || count1 == MAX_ITERS) {
@@ -388,7 +459,8 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, 
             hg = hnew;
             C->hg = hg;
             C->count1 = count1 + 1;
-            V[V_Y * WAVE + lane] = hg * z1in + z0;
+#pragma unroll
+            FOR_S V[V_Y * VW + CS] = hg * z1in[s] + z0[s];
             return A_RHS;
         }
         double h0 = H_BIAS * hnew;
@@ -401,10 +473,11 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, double f, 
     const double tn = ud(C->tn), tstop = ud(C->tstop);
     if ((tn + h - tstop) * h > 0.0) h = (tstop - tn) * (1.0 - 4.0 * UROUND);
     C->h = h; C->hscale = h; C->hprime = h;
-    trace_row(C, a, lane, 0, 0.0, z0);
-    V[WAVE + lane] *= h;
+    trace_row<CPL>(C, a, lane, 0, 0.0, z0, z0);
+#pragma unroll
+    FOR_S V[VW + CS] *= h;
     if (a.max_steps <= 0) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
-    begin_step(C, V, lane, a);
+    begin_step<CPL>(C, V, lane, a);
     C->phase = PH_NEWTON;
     return A_RHS;
 }
@@ -435,28 +508,34 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 // Controller, part 2: after the linear solve (delta = this lane's Newton correction) or after
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
-__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double delta, int lu_fail) {
+template <int CPL>
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (&delta)[CPL], int lu_fail) {
+    constexpr int VW = 64 * CPL;
     const CtlArgs a = load_args(C);
     const int n = a.n;
-    const bool act = lane < n;
-    const double ewt = V[V_EWT * WAVE + lane];
+    double ewt[CPL], acor[CPL];
+#pragma unroll
+    FOR_S ewt[s] = V[V_EWT * VW + CS];
     int nls;                                                   // 0 converged, else failure
     if (lu_fail) {
         nls = 2;
     } else {
         C->nni = ui(C->nni) + 1;
         const double gamrat = ud(C->gamrat);
-        if (gamrat != 1.0) delta *= 2.0 / (1.0 + gamrat);
-        const double acor = V[V_ACOR * WAVE + lane] + delta;
-        V[V_ACOR * WAVE + lane] = acor;
-        const double del = wrms_l(delta, ewt, lane, n);     // cvNlsConvTest
+#pragma unroll
+        FOR_S {
+            if (gamrat != 1.0) delta[s] *= 2.0 / (1.0 + gamrat);
+            acor[s] = V[V_ACOR * VW + CS] + delta[s];
+            V[V_ACOR * VW + CS] = acor[s];
+        }
+        const double del = wrms_l<CPL>(delta, ewt, lane, n);     // cvNlsConvTest
         const int m = ui(C->m_it);
         double crate = ud(C->crate);
         const double delp = ud(C->delp);
         if (m > 0) { crate = fmax(CRDOWN * crate, del / delp); C->crate = crate; }
         const double dcon = del * fmin(1.0, crate) / ud(C->tol);
         if (dcon <= 1.0) {
-            C->acnrm = (m == 0) ? del : wrms_l(acor, ewt, lane, n);
+            C->acnrm = (m == 0) ? del : wrms_l<CPL>(acor, ewt, lane, n);
             nls = 0;
         } else {
             bool fail = (m >= 1) && (del > RDIV * delp);
@@ -466,13 +545,17 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
                 if (m + 1 >= NLS_MAXCOR) fail = true;
             }
             if (!fail) {
-                V[V_Y * WAVE + lane] = V[lane] + acor;
+#pragma unroll
+                FOR_S V[V_Y * VW + CS] = V[CS] + acor[s];
                 return A_RHS;
             }
             if (!ui(C->jcur_nls)) {                          // retry with a fresh Jacobian
                 C->callSetup = 1; C->jbad = 1; C->m_it = 0;
-                V[V_ACOR * WAVE + lane] = 0.0;
-                V[V_Y * WAVE + lane] = V[lane];
+#pragma unroll
+                FOR_S {
+                    V[V_ACOR * VW + CS] = 0.0;
+                    V[V_Y * VW + CS] = V[CS];
+                }
                 return A_RHS;
             }
             nls = 1;
@@ -480,14 +563,14 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
     }
     if (nls != 0) {                                          // cvHandleNFlag
         C->ncfn = ui(C->ncfn) + 1;
-        cv_restore(C, V, lane);
+        cv_restore<CPL>(C, V, lane);
         const int ncf = ui(C->ncf) + 1;
         C->ncf = ncf;
         C->etamax = 1.0;
         if (ncf == MXNCF) { C->status = BR_ERR_CONV; return A_DONE; }
         C->eta = ETACF;
-        cv_rescale(C, V, lane);
-        begin_attempt(C, V, lane, PREV_CONV_FAIL);
+        cv_rescale<CPL>(C, V, lane);
+        begin_attempt<CPL>(C, V, lane, PREV_CONV_FAIL);
         return A_RHS;
     }
     // ---- cvDoErrorTest
@@ -496,7 +579,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
     if (dsm > 1.0) {
         const int nef = ui(C->nef) + 1;
         C->nef = nef; C->netf = ui(C->netf) + 1;
-        cv_restore(C, V, lane);
+        cv_restore<CPL>(C, V, lane);
         if (nef == MXNEF) { C->status = BR_ERR_ERRTEST; return A_DONE; }
         C->etamax = 1.0;
         if (nef <= MXNEF1) {
@@ -504,22 +587,23 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
             eta = fmax(ETAMIN, eta);
             if (nef >= SMALL_NEF) eta = fmin(eta, ETAMXF);
             C->eta = eta;
-            cv_rescale(C, V, lane);
-            begin_attempt(C, V, lane, PREV_ERR_FAIL);
+            cv_rescale<CPL>(C, V, lane);
+            begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
             return A_RHS;
         }
         if (q > 1) {
             C->eta = ETAMIN;
-            cv_adjust_order(C, V, lane, -1);
+            cv_adjust_order<CPL>(C, V, lane, -1);
             C->L = q; C->q = q - 1; C->qwait = q;
-            cv_rescale(C, V, lane);
-            begin_attempt(C, V, lane, PREV_ERR_FAIL);
+            cv_rescale<CPL>(C, V, lane);
+            begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
             return A_RHS;
         }
         C->eta = ETAMIN;
         const double h = ud(C->h) * ETAMIN;
         C->h = h; C->hscale = h; C->qwait = LONG_WAIT;
-        V[V_Y * WAVE + lane] = V[lane];
+#pragma unroll
+        FOR_S V[V_Y * VW + CS] = V[CS];
         C->phase = PH_EF1;
         return A_RHS;
     }
@@ -530,11 +614,22 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
     for (int i = q; i >= 2; --i) C->tau[i] = ud(C->tau[i - 1]);
     if ((q == 1) && (nst > 1)) C->tau[2] = ud(C->tau[1]);
     C->tau[1] = h;
-    const double acor = V[V_ACOR * WAVE + lane];
 #pragma unroll
-    for (int j = 0; j <= QMAX; ++j) if (j <= q) V[j * WAVE + lane] += ud(C->l[j]) * acor;
+    FOR_S acor[s] = V[V_ACOR * VW + CS];
+#pragma unroll
+    for (int j = 0; j <= QMAX; ++j) {
+        if (j <= q) {
+            const double lj = ud(C->l[j]);
+#pragma unroll
+            FOR_S V[j * VW + CS] += lj * acor[s];
+        }
+    }
     int qwait = ui(C->qwait) - 1;
-    if ((qwait == 1) && (q != QMAX)) { V[QMAX * WAVE + lane] = acor; C->saved_tq5 = ud(C->tq[5]); }
+    if ((qwait == 1) && (q != QMAX)) {
+#pragma unroll
+        FOR_S V[QMAX * VW + CS] = acor[s];
+        C->saved_tq5 = ud(C->tq[5]);
+    }
     // ---- cvPrepareNextStep
     double eta = 1.0, hprime = h;
     int qprime = q;
@@ -549,21 +644,30 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
             qwait = 2;
             double etaqm1 = 0.0, etaqp1 = 0.0;
             if (q > 1) {
-                const double ddn = wrms_l(V[q * WAVE + lane], ewt, lane, n) * ud(C->tq[1]);
+                double zq[CPL];
+#pragma unroll
+                FOR_S zq[s] = V[q * VW + CS];
+                const double ddn = wrms_l<CPL>(zq, ewt, lane, n) * ud(C->tq[1]);
                 etaqm1 = 1.0 / (root_int(BIAS1 * ddn, q) + ADDON);
             }
             const double saved_tq5 = ud(C->saved_tq5);
             if (q != QMAX && saved_tq5 != 0.0) {
                 const double cquot = (ud(C->tq[5]) / saved_tq5) * pow_int(h / ud(C->tau[2]), L);
-                const double tempv = acor - cquot * V[QMAX * WAVE + lane];
-                const double dup = wrms_l(tempv, ewt, lane, n) * ud(C->tq[3]);
+                double tempv[CPL];
+#pragma unroll
+                FOR_S tempv[s] = acor[s] - cquot * V[QMAX * VW + CS];
+                const double dup = wrms_l<CPL>(tempv, ewt, lane, n) * ud(C->tq[3]);
                 etaqp1 = 1.0 / (root_int(BIAS3 * dup, L + 1) + ADDON);
             }
             const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
             if (etam < THRESH) { eta = 1.0; }
             else if (etam == etaq) { eta = etaq; }
             else if (etam == etaqm1) { eta = etaqm1; qprime = q - 1; }
-            else { eta = etaqp1; qprime = q + 1; V[QMAX * WAVE + lane] = acor; }
+            else {
+                eta = etaqp1; qprime = q + 1;
+#pragma unroll
+                FOR_S V[QMAX * VW + CS] = acor[s];
+            }
         }
         if (eta < THRESH) { eta = 1.0; hprime = h; }                // cvSetEta
         else {
@@ -574,15 +678,27 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
     }
     C->qwait = qwait;
     C->etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-    V[V_ACOR * WAVE + lane] = acor * ud(C->tq[2]);
+    const double tq2 = ud(C->tq[2]);
+#pragma unroll
+    FOR_S V[V_ACOR * VW + CS] = acor[s] * tq2;
     const int nstloc = ui(C->nstloc) + 1;
     C->nstloc = nstloc;
     const double tn = ud(C->tn);
-    const double z0 = V[lane];
+    double z0[CPL];
+#pragma unroll
+    FOR_S z0[s] = V[CS];
     C->eta = eta; C->hprime = hprime; C->qprime = qprime;
-    trace_row(C, a, lane, nst, tn, z0);
+    if (a.trace) {
+        double yl[CPL];
+#pragma unroll
+        FOR_S yl[s] = V[V_Y * VW + CS];                     // the last RHS was evaluated at y
+        trace_row<CPL>(C, a, lane, nst, tn, z0, yl);
+    }
     if (a.ufac > 0.0) {                                      // runaway state (br_opts.unstable_factor)
-        const double mx = uni(wave_max(act ? fabs(z0) : 0.0));
+        double zm = 0.0;
+#pragma unroll
+        FOR_S if (CS < n) zm = fmax(zm, fabs(z0[s]));
+        const double mx = uni(wave_max(zm));
         if (!(mx <= ud(C->ulimit))) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
     }
     // CVode ONE_STEP + tstop handling
@@ -590,13 +706,16 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
     if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
         const double sk = (tstop - tn) / h;
-        double yv = V[q * WAVE + lane];
-        for (int j = q - 1; j >= 0; --j) yv = V[j * WAVE + lane] + sk * yv;
-        V[V_Y * WAVE + lane] = yv;
-        if (a.trace && nst <= a.trace_cap) {
-            double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + nst) * (n + 4);
-            if (lane == 0) row[0] = tstop;
-            if (act) row[4 + lane] = yv;
+#pragma unroll
+        FOR_S {
+            double yv = V[q * VW + CS];
+            for (int j = q - 1; j >= 0; --j) yv = V[j * VW + CS] + sk * yv;
+            V[V_Y * VW + CS] = yv;
+            if (a.trace && nst <= a.trace_cap) {
+                double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + nst) * (2 * n + 4);
+                if (lane == 0 && s == 0) row[0] = tstop;
+                if (CS < n) row[4 + CS] = yv;
+            }
         }
         return A_DONE;
     }
@@ -606,7 +725,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double d
         C->eta = hprime / h;
     }
     if (nstloc >= a.max_steps) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
-    begin_step(C, V, lane, a);
+    begin_step<CPL>(C, V, lane, a);
     return A_RHS;
 }
 
@@ -621,8 +740,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     DevMech M, int N, int rpb, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
     const double* __restrict__ tfv, KOpts o, double* __restrict__ stats, double* __restrict__ Jws,
     double* __restrict__ trace) {
+    constexpr int CPL = NMAX > 64 ? 2 : 1;   // components per lane
+    constexpr int VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
@@ -632,25 +753,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     LDbl* V = (LDbl*)(smem_raw + roff + CTL_BYTES);
     const RView& S = W.R;
     const int n = M.n;
-    const bool act = lane < n;
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
     double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
-    double* LUsave = Jsave + NMAX * WAVE;
+    double* LUsave = Jsave + NMAX * VW;
     double* jscr = LUsave + lu_ws_doubles(NMAX);
     C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
     C->a_max_steps = o.max_steps; C->a_trace_cap = o.trace_cap; C->a_trace = trace; C->a_rid = rid; C->a_n = n;
 
-    init_tconst(M, tb, S, T, lane);
+    init_tconst<CPL>(M, tb, S, T, lane);
 
     // ---- CVodeInit
-    const double u0 = act ? U[(size_t)rid * n + lane] : 0.0;
+    double u0[CPL], su = 0.0;
 #pragma unroll
-    for (int j = 0; j < NVEC; ++j) V[j * WAVE + lane] = 0.0;
-    V[lane] = u0;
-    V[V_Y * WAVE + lane] = u0;
-    V[V_EWT * WAVE + lane] = act ? 1.0 / (o.rtol * fabs(u0) + o.atol) : 1.0;
+    FOR_S {
+        const bool act = CS < n;
+        u0[s] = act ? U[(size_t)rid * n + CS] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NVEC; ++j) V[j * VW + CS] = 0.0;
+        V[CS] = u0[s];
+        V[V_Y * VW + CS] = u0[s];
+        V[V_EWT * VW + CS] = act ? 1.0 / (o.rtol * fabs(u0[s]) + o.atol) : 1.0;
+        su += act ? fabs(u0[s]) : 0.0;
+    }
 #pragma unroll
     for (int i = 0; i < QMAX + 2; ++i) C->tau[i] = 0.0;
 #pragma unroll
@@ -661,7 +787,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     C->delp = 0.0; C->hprime = 0.0; C->hscale = 0.0; C->eta = 1.0; C->etamax = ETAMX1; C->acnrm = 0.0;
     C->saved_tq5 = 0.0; C->saved_t = 0.0; C->tol = 0.0; C->hg = 0.0; C->hub = 0.0; C->hlb = 0.0; C->hnew = 0.0;
     C->tstop = tfv[rid];
-    C->ulimit = o.ufac * uni(wave_sum(act ? fabs(u0) : 0.0));
+    C->ulimit = o.ufac * uni(wave_sum(su));
     C->q = 1; C->qprime = 1; C->L = 2; C->qwait = 2;
     C->nst = 0; C->nfe = 0; C->nsetups = 0; C->nje = 0; C->nni = 0; C->ncfn = 0; C->netf = 0; C->nstlp = 0;
     C->nstlj = 0; C->ncf = 0; C->nef = 0; C->nstloc = 0; C->status = 0; C->m_it = 0; C->convfail = 0;
@@ -678,19 +804,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
 #define BR_ACC(acc, v)
 #endif
     const unsigned long long cyc0 = wall_clock64();
-    int perm = lane;
+    int perm[CPL];
+#pragma unroll
+    FOR_S perm[s] = CS;
+    LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // LU scratch (CPL = 2): the production sums are idle then
     double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
     for (;;) {
-        const double y = V[V_Y * WAVE + lane];
-        double f;
+        double y[CPL], f[CPL];
+#pragma unroll
+        FOR_S y[s] = V[V_Y * VW + CS];
         {
             BR_CLK(c0);
-            f = rhs(M, tb, S, T, Asv, Asv_th, y, lane, p_last);
+            rhs<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, p_last, f);
             BR_ACC(cyc_rhs, c0);
         }
-        double b = 0.0;
+        double b[CPL];
         BR_CLK(c2);
-        int act_code = ctl_post_rhs(C, V, lane, f, &b);
+        int act_code = ctl_post_rhs<CPL>(C, V, lane, f, b);
         BR_ACC(cyc_ctl, c2);
         if (act_code == A_RHS) continue;
         if (act_code == A_DONE) break;
@@ -698,27 +828,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
         if (act_code == A_SETUP) {
             if (ui(C->newj)) {
                 BR_CLK(c0);
-                jacobian(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
+                jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm);
+            if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
+            else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
         }
-        double delta = 0.0;
+        double delta[CPL];
+#pragma unroll
+        FOR_S delta[s] = 0.0;
         if (!lu_fail) {
             BR_CLK(c0);
-            delta = lu_solve<NMAX>(LUsave, n, lane, perm, b);
+            if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0]);
+            else {
+                lu_solve2<NMAX>(LUsave, scr, n, lane, perm, b);
+                delta[0] = b[0];
+                delta[1] = b[1];
+            }
             BR_ACC(cyc_sol, c0);
         }
         BR_CLK(c3);
-        act_code = ctl_post_solve(C, V, lane, delta, lu_fail);
+        act_code = ctl_post_solve<CPL>(C, V, lane, delta, lu_fail);
         BR_ACC(cyc_ctl, c3);
         if (act_code == A_DONE) break;
     }
     const int status = ui(C->status);
-    const double u_out = status ? V[lane] : V[V_Y * WAVE + lane];
-    if (act) U[(size_t)rid * n + lane] = u_out;
+#pragma unroll
+    FOR_S {
+        const double u_out = status ? V[CS] : V[V_Y * VW + CS];
+        if (CS < n) U[(size_t)rid * n + CS] = u_out;
+    }
     if (stats && lane == 0) {
         double* st = stats + (size_t)rid * BR_NSTAT;
         st[0] = (double)ui(C->nst); st[1] = (double)ui(C->nfe); st[2] = (double)ui(C->nje);
@@ -738,36 +879,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
 // ------------------------------------------------------------------------------------
 // parity kernels: rates, rhs, jacobian (one reactor per wave)
 // ------------------------------------------------------------------------------------
+template <int CPL>
 __global__ __launch_bounds__(256) void k_rates(DevMech M, int N, int rpb, const double* Tv, const double* pv,
                                                const double* X, const double* TH, double* W_, double* SD) {
+    typedef Lay<CPL> L;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
     const RView& S = W.R;
     const double T = Tv[rid], p = pv[rid];
-    init_tconst(M, W.tb, S, T, lane);
-    double c = 0.0;
-    if (lane < M.ng) c = p * X[(size_t)rid * M.ng + lane] / (R_GAS * T);
-    else if (lane < M.n) c = TH ? TH[(size_t)rid * M.ns + (lane - M.ng)] : 0.0;
-    if (lane < M.n) { S.sp[SP_CONC + lane] = c; S.sp[SP_ACCW + lane] = 0.0; S.sp[SP_ACCS + lane] = 0.0; }
-    const double Ctot = wave_sum(lane < M.ng ? c : 0.0);
+    init_tconst<CPL>(M, W.tb, S, T, lane);
+    double cg = 0.0;
+#pragma unroll
+    FOR_S {
+        const int k = CS;
+        double c = 0.0;
+        if (k < M.ng) c = p * X[(size_t)rid * M.ng + k] / (R_GAS * T);
+        else if (k < M.n) c = TH ? TH[(size_t)rid * M.ns + (k - M.ng)] : 0.0;
+        if (k < M.n) { S.sp[L::CONC + k] = c; S.sp[L::ACCW + k] = 0.0; S.sp[L::ACCS + k] = 0.0; }
+        cg += k < M.ng ? c : 0.0;
+    }
+    const double Ctot = wave_sum(cg);
     wave_sync();
-    third_body_sets(M, W.tb, S.sp, Ctot, lane);
+    third_body_sets<CPL>(M, W.tb, S.sp, Ctot, lane);
     wave_sync();
-    production(M, W.tb, S, R_GAS * T, lane);
+    production<CPL>(M, W.tb, S, R_GAS * T, lane);
     wave_sync();
-    const double w = lane < M.n ? S.sp[SP_ACCW + lane] : 0.0;
-    const double s = lane < M.n ? S.sp[SP_ACCS + lane] : 0.0;
-    if (lane < M.ng) W_[(size_t)rid * M.ng + lane] = w;
-    if (SD && lane < M.n) SD[(size_t)rid * M.n + lane] = s;
+#pragma unroll
+    FOR_S {
+        const int k = CS;
+        const double w = k < M.n ? S.sp[L::ACCW + k] : 0.0;
+        const double sd = k < M.n ? S.sp[L::ACCS + k] : 0.0;
+        if (k < M.ng) W_[(size_t)rid * M.ng + k] = w;
+        if (SD && k < M.n) SD[(size_t)rid * M.n + k] = sd;
+    }
 }
 
+template <int CPL>
 __global__ __launch_bounds__(256) void k_rhs(DevMech M, int N, int rpb, const double* Tv, const double* Asvv,
                                              const double* U, double* DU) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
@@ -775,18 +929,21 @@ __global__ __launch_bounds__(256) void k_rhs(DevMech M, int N, int rpb, const do
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
-    init_tconst(M, W.tb, S, T, lane);
-    const bool act = lane < M.n;
-    const double u = act ? U[(size_t)rid * M.n + lane] : 0.0;
-    const double du = rhs(M, W.tb, S, T, Asv, Asv_th, u, lane, reinterpret_cast<double*>(W.rbase));
-    if (act) DU[(size_t)rid * M.n + lane] = du;
+    init_tconst<CPL>(M, W.tb, S, T, lane);
+    double u[CPL], du[CPL];
+#pragma unroll
+    FOR_S u[s] = CS < M.n ? U[(size_t)rid * M.n + CS] : 0.0;
+    rhs<CPL>(M, W.tb, S, T, Asv, Asv_th, u, lane, reinterpret_cast<double*>(W.rbase), du);
+#pragma unroll
+    FOR_S if (CS < M.n) DU[(size_t)rid * M.n + CS] = du[s];
 }
 
 template <int NMAX>
 __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const double* Tv, const double* Asvv,
                                              const double* U, double* J, double* Jws) {
+    constexpr int CPL = NMAX > 64 ? 2 : 1, VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
@@ -794,15 +951,18 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
-    init_tconst(M, W.tb, S, T, lane);
-    const bool act = lane < M.n;
-    const double u = act ? U[(size_t)rid * M.n + lane] : 0.0;
-    double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);
-    jacobian(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * WAVE + lu_ws_doubles(NMAX));
-    if (act) {
-        double* row = J + ((size_t)rid * M.n + lane) * M.n;
+    init_tconst<CPL>(M, W.tb, S, T, lane);
+    double u[CPL];
 #pragma unroll
-        for (int j = 0; j < NMAX; ++j) if (j < M.n) row[j] = Jsave[j * WAVE + lane];
+    FOR_S u[s] = CS < M.n ? U[(size_t)rid * M.n + CS] : 0.0;
+    double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);
+    jacobian<CPL>(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * VW + lu_ws_doubles(NMAX));
+#pragma unroll
+    FOR_S {
+        if (CS < M.n) {
+            double* row = J + ((size_t)rid * M.n + CS) * M.n;
+            for (int j = 0; j < M.n; ++j) row[j] = Jsave[j * VW + CS];
+        }
     }
 }
 
@@ -870,13 +1030,17 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     if (!d || !out) return fail(BR_ERR_INPUT, "null argument");
     const int ng = d->ng, ns = d->ns, nrg = d->nrg, nrs = d->nrs, n = ng + ns;
     if (ng <= 0 || ns < 0 || nrg < 0 || nrs < 0) return fail(BR_ERR_INPUT, "bad sizes");
-    if (n > 64) return fail(BR_ERR_UNSUPPORTED, "n > 64 components is not supported by this build");
+    if (n > 72) return fail(BR_ERR_UNSUPPORTED, "n > 72 components is not supported by this build");
     HIPCHK(hipSetDevice(device));
     br_mech* m = new br_mech();
     m->device = device; m->ng = ng; m->ns = ns; m->nrg = nrg; m->nrs = nrs; m->n = n;
-    m->nmax = n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : 64));
+    m->nmax = n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : (n <= 64 ? 64 : 72)));
     DevMech& M = m->dm;
     M.ng = ng; M.ns = ns; M.n = n; M.nrg = nrg; M.nrs = nrs; M.conv = d->conv;
+    M.cpl = n > 64 ? 2 : 1;
+    const int SPW = 64 * M.cpl;                                   // species slots (Lay<CPL>::SPW)
+    const int SP_ONE = M.cpl == 2 ? Lay<2>::ONE : Lay<1>::ONE;    // pad species: conc = 1
+    const int IMG_RX_OFF = M.cpl == 2 ? Lay<2>::IMG_RX : Lay<1>::IMG_RX;
     M.p_std = d->p_std > 0 ? d->p_std : 1e5;
     M.G = d->site_density * 1e4;
     auto pack4 = [](const int* v, int cnt, int pad = 255) {
@@ -1027,7 +1191,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         }
         colptr.push_back((int)colrx.size());
     }
-    // ---- LDS table image: molwt[64] | sigma[64] | RX | SX | SXE | TBE
+    // ---- LDS table image: molwt[SPW] | sigma[SPW] | RX | SX | SXE | TBE
     auto al16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     size_t off = IMG_RX_OFF + al16(RX_WORDS * 4 * (size_t)nrg);
     M.sx_off = (int)off;
@@ -1042,9 +1206,9 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     std::vector<unsigned char> img(M.img_bytes, 0);
     {
         double* mw = reinterpret_cast<double*>(img.data());
-        for (int k = 0; k < 64; ++k) { mw[k] = 1.0; mw[64 + k] = 1.0; }
+        for (int k = 0; k < SPW; ++k) { mw[k] = 1.0; mw[SPW + k] = 1.0; }
         for (int k = 0; k < ng; ++k) mw[k] = d->molwt[k];
-        for (int i = 0; i < ns; ++i) mw[64 + ng + i] = d->sigma ? d->sigma[i] : 1.0;
+        for (int i = 0; i < ns; ++i) mw[SPW + ng + i] = d->sigma ? d->sigma[i] : 1.0;
         if (nrg) memcpy(img.data() + IMG_RX_OFF, rx.data(), rx.size() * 4);
         if (nrs) memcpy(img.data() + M.sx_off, sx.data(), sx.size() * 4);
         if (nrs) memcpy(img.data() + M.sxe_off, sxe.data(), sxe.size() * 8);
@@ -1058,7 +1222,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     }
     M.fod_off = fod_off_bytes(nrg);
     M.skd_off = skd_off_bytes(nrg, nfo);
-    M.rblock_bytes = rblock_bytes(nrg, nfo, nrs);
+    M.rblock_bytes = rblock_bytes(nrg, nfo, nrs, M.cpl);
     std::vector<double> nasa((size_t)ng * 15);
     for (size_t i = 0; i < (size_t)ng * 15; ++i) nasa[i] = d->nasa[i];
     if (tbeff.empty()) tbeff.push_back(0.0);
@@ -1076,7 +1240,8 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     //      per reactor); ties go to the smaller workgroup
     const void* kfn = m->nmax == 16 ? (const void*)k_integrate<16>
                     : m->nmax == 32 ? (const void*)k_integrate<32>
-                    : m->nmax == 56 ? (const void*)k_integrate<56> : (const void*)k_integrate<64>;
+                    : m->nmax == 56 ? (const void*)k_integrate<56>
+                    : m->nmax == 64 ? (const void*)k_integrate<64> : (const void*)k_integrate<72>;
     int best = 0, best_w = 0;
     for (int rpb = 1; rpb <= 4; ++rpb) {
         const size_t b = wg_lds_bytes(M, rpb);
@@ -1147,8 +1312,13 @@ int br_rates(br_mech* m, int N, const double* T, const double* p, const double* 
     HIPCHK(hipMemcpy(dx, x, (size_t)N * ng * sizeof(double), hipMemcpyHostToDevice));
     if (ns && theta) HIPCHK(hipMemcpy(dth, theta, (size_t)N * ns * sizeof(double), hipMemcpyHostToDevice));
     else if (ns) HIPCHK(hipMemset(dth, 0, (size_t)N * ns * sizeof(double)));
-    HIPCHK(hipFuncSetAttribute((const void*)k_rates, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-    hipLaunchKernelGGL(k_rates, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds);
+    if (m->dm.cpl == 2) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_rates<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
+        hipLaunchKernelGGL(k_rates<2>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds);
+    } else {
+        HIPCHK(hipFuncSetAttribute((const void*)k_rates<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
+        hipLaunchKernelGGL(k_rates<1>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(wdot, dw, (size_t)N * ng * sizeof(double), hipMemcpyDeviceToHost));
     if (sdot) HIPCHK(hipMemcpy(sdot, ds, (size_t)N * n * sizeof(double), hipMemcpyDeviceToHost));
@@ -1169,8 +1339,13 @@ int br_rhs(br_mech* m, int N, const double* T, const double* Asv, const double* 
     HIPCHK(hipMemcpy(dT, T, N * sizeof(double), hipMemcpyHostToDevice));
     if (Asv) HIPCHK(hipMemcpy(dA, Asv, N * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(du_, u, (size_t)N * n * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipFuncSetAttribute((const void*)k_rhs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-    hipLaunchKernelGGL(k_rhs, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu);
+    if (m->dm.cpl == 2) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_rhs<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
+        hipLaunchKernelGGL(k_rhs<2>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu);
+    } else {
+        HIPCHK(hipFuncSetAttribute((const void*)k_rhs<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
+        hipLaunchKernelGGL(k_rhs<1>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(du, ddu, (size_t)N * n * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
@@ -1193,8 +1368,13 @@ int br_jacobian(br_mech* m, int N, const double* T, const double* Asv, const dou
     const double* pA = Asv ? dA : nullptr;
     rc = ensure_jws(m, N);
     if (rc) return rc;
-    HIPCHK(hipFuncSetAttribute((const void*)k_jac<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-    hipLaunchKernelGGL(k_jac<64>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, pA, du_, dJ, m->jws);
+    if (m->dm.cpl == 2) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_jac<72>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
+        hipLaunchKernelGGL(k_jac<72>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, pA, du_, dJ, m->jws);
+    } else {
+        HIPCHK(hipFuncSetAttribute((const void*)k_jac<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
+        hipLaunchKernelGGL(k_jac<64>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, pA, du_, dJ, m->jws);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(J, dJ, (size_t)N * n * n * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
@@ -1227,9 +1407,12 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     } else if (m->nmax == 56) {
         HIPCHK(hipFuncSetAttribute((const void*)k_integrate<56>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem));
         hipLaunchKernelGGL(k_integrate<56>, grid, block, m->shmem, s, m->dm, N, rpb, dT, dAsv, du, dtf, o, (double*)dstats, m->jws, trace);
-    } else {
+    } else if (m->nmax == 64) {
         HIPCHK(hipFuncSetAttribute((const void*)k_integrate<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem));
         hipLaunchKernelGGL(k_integrate<64>, grid, block, m->shmem, s, m->dm, N, rpb, dT, dAsv, du, dtf, o, (double*)dstats, m->jws, trace);
+    } else {
+        HIPCHK(hipFuncSetAttribute((const void*)k_integrate<72>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem));
+        hipLaunchKernelGGL(k_integrate<72>, grid, block, m->shmem, s, m->dm, N, rpb, dT, dAsv, du, dtf, o, (double*)dstats, m->jws, trace);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(m->ev1, s));
@@ -1259,7 +1442,7 @@ static int integrate_host(br_mech* m, int N, const double* T, const double* Asv,
     const int n = m->n;
     const int cap = (trace && opts) ? opts->trace_cap : 0;
     if (trace && cap <= 0) return fail(BR_ERR_INPUT, "trace_cap must be > 0");
-    const size_t ntr = trace ? (size_t)N * (cap + 1) * (n + 4) : 0;
+    const size_t ntr = trace ? (size_t)N * (cap + 1) * (2 * n + 4) : 0;
     const size_t nd = (size_t)N * (3 + n + BR_NSTAT) + ntr;
     int rc = ensure_ws(m, nd * sizeof(double));
     if (rc) return rc;
@@ -1319,19 +1502,46 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     if (lane < n) x[(size_t)rid * n + lane] = r;
     if (lane == 0) fail[rid] = f;
 }
+template <int NMAX>
+__global__ __launch_bounds__(64) void k_lu_check2(int N, int n, const double* J, const double* g, const double* b,
+                                                  double* x, double* ws, int* fail) {
+    constexpr int JW = 128;
+    __shared__ double scr[192];
+    const int rid = blockIdx.x;
+    if (rid >= N) return;
+    const int lane = threadIdx.x;
+    double* Jt = ws + (size_t)rid * (NMAX * JW + lu_ws_doubles(NMAX));
+    double* LU = Jt + NMAX * JW;
+    for (int j = 0; j < NMAX; ++j)
+        for (int s = 0; s < 2; ++s) {
+            const int row = lane + 64 * s;
+            Jt[j * JW + row] = (row < n && j < n) ? J[((size_t)rid * n + row) * n + j] : 0.0;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    int perm[2] = {lane, lane + 64};
+    const int f = lu_factor2<NMAX>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    double r[2];
+    for (int s = 0; s < 2; ++s) r[s] = (lane + 64 * s < n) ? b[(size_t)rid * n + lane + 64 * s] : 0.0;
+    lu_solve2<NMAX>(LU, (LDSd*)scr, n, lane, perm, r);
+    for (int s = 0; s < 2; ++s) if (lane + 64 * s < n) x[(size_t)rid * n + lane + 64 * s] = r[s];
+    if (lane == 0) fail[rid] = f;
+}
 }  // namespace
 
 extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* gamma, const double* b, double* x,
                                  int* fail_out) {
-    if (N <= 0 || n <= 0 || n > 64) return fail_code_input();
-    const int nmax = n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : 64));
+    if (N <= 0 || n <= 0 || n > 72) return fail_code_input();
+    const int nmax = n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : (n <= 64 ? 64 : 72)));
     double *dJ, *dg, *db, *dx, *dws;
     int* df;
     HIPCHK(hipMalloc(&dJ, (size_t)N * n * n * 8));
     HIPCHK(hipMalloc(&dg, (size_t)N * 8));
     HIPCHK(hipMalloc(&db, (size_t)N * n * 8));
     HIPCHK(hipMalloc(&dx, (size_t)N * n * 8));
-    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * WAVE + lu_ws_doubles(nmax)) * 8));
+    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
     HIPCHK(hipMalloc(&df, (size_t)N * 4));
     HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
@@ -1339,7 +1549,8 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     if (nmax == 16) hipLaunchKernelGGL(k_lu_check<16>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
     else if (nmax == 32) hipLaunchKernelGGL(k_lu_check<32>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
     else if (nmax == 56) hipLaunchKernelGGL(k_lu_check<56>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
-    else hipLaunchKernelGGL(k_lu_check<64>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
+    else if (nmax == 64) hipLaunchKernelGGL(k_lu_check<64>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
+    else hipLaunchKernelGGL(k_lu_check2<72>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(x, dx, (size_t)N * n * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));

@@ -18,6 +18,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace brhip {
 
@@ -30,6 +31,7 @@ constexpr int WAVE = 64;
 struct DevMech {
     int ng, ns, n, nrg, nrs, ntb, nfo, ntbe, nset, conv;
     int nu4;                      // some gas reaction has 4 reactants or 4 products
+    int cpl;                      // components per lane: 1 (n <= 64) or 2 (64 < n <= 128), see Lay
     double p_std, G;              // Pa ; site density mol/m2
     const uint4* img;             // LDS table image (global copy)
     int img_bytes;                // multiple of 16
@@ -82,23 +84,36 @@ __host__ __device__ inline int si_ncov(uint32_t v) { return (v >> 7) & 7; }
 __host__ __device__ inline int si_gas(uint32_t v) { return (v >> 10) & 255; }
 __host__ __device__ inline int sp8(uint32_t w, int e) { return (w >> (8 * e)) & 255; }
 constexpr int RX_WORDS = 8, SX_WORDS = 12, SXE_DOUBLES = 8;
-constexpr int IMG_RX_OFF = 1024;
+
+// Components per lane: CPL = 1 for n <= 64 (lane k <-> component k); CPL = 2 for 64 < n <= 128
+// (lane k <-> components k and k + 64, e.g. GRI gas + Ni surface, n = 66). Species-indexed LDS
+// arrays and the table image are sized SPW = 64 * CPL.
+template <int CPL>
+struct Lay {
+    static constexpr int SPW = 64 * CPL;
+    // species block (doubles): conc[SPW], conc[ONE] = 1.0 (pad species of the packed records),
+    // accw[SPW], accs[SPW], mc[64] third-body concentration per efficiency set
+    static constexpr int CONC = 0, ONE = SPW, ACCW = SPW + 16, ACCS = 2 * SPW + 16, MC = 3 * SPW + 16;
+    static constexpr int DOUBLES = 3 * SPW + 16 + 64, BYTES = DOUBLES * 8;
+    static constexpr int IMG_RX = 16 * SPW;   // image: molwt[SPW] | sigma[SPW] | RX records ...
+};
 
 struct Tab {   // views of the staged table image
-    const double* molwt;   // [64]
-    const double* sigma;   // [64]
+    const double* molwt;   // [SPW]
+    const double* sigma;   // [SPW]
     const uint32_t* rx;    // RX_WORDS per gas reaction
     const uint32_t* sx;    // SX_WORDS per surface reaction
     const double* sxe;     // SXE_DOUBLES per surface reaction: coverage eps[4], site factor, pad
     const char* tbe;       // 16 B per third-body entry
     const uint32_t* tbs;   // per efficiency set: start | count << 20 into tbe
 };
+template <int CPL>
 __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
     Tab t;
     base = br_lds;
     t.molwt = reinterpret_cast<const double*>(base);
-    t.sigma = t.molwt + 64;
-    t.rx = reinterpret_cast<const uint32_t*>(base + IMG_RX_OFF);
+    t.sigma = t.molwt + Lay<CPL>::SPW;
+    t.rx = reinterpret_cast<const uint32_t*>(base + Lay<CPL>::IMG_RX);
     t.sx = reinterpret_cast<const uint32_t*>(base + MF(sx_off));
     t.sxe = reinterpret_cast<const double*>(base + MF(sxe_off));
     t.tbe = base + MF(tbe_off);
@@ -181,26 +196,23 @@ __device__ __forceinline__ int launder_v(int v) {
 // per-reactor rate workspace (LDS)
 // ------------------------------------------------------------------------------------
 struct RView {
-    double* sp;    // species block: conc[k] = sp[SP_CONC+k], accw, accs, mc (see SP_* offsets)
+    double* sp;    // species block: conc[k] = sp[CONC+k], accw, accs, mc (see Lay)
     double* rxd;   // kf = rxd[2r], kr = rxd[2r+1]
     double* fod;   // k0, log10 Fcent, c, n per falloff reaction
     double* skd;   // k(T), k*exp(-sum eps theta/RT) (Jacobian) per surface reaction
 };
-// species block (doubles): conc[0..63], conc[SP_ONE] = 1.0 (pad species), accw[64], accs[64],
-// mc[64] third-body concentration per efficiency set
-constexpr int SP_CONC = 0, SP_ONE = 64, SP_ACCW = 80, SP_ACCS = 144, SP_MC = 208, SP_DOUBLES = 272;
-constexpr int SP_BYTES = SP_DOUBLES * 8;
 __host__ __device__ inline int fod_off_bytes(int nrg) { return (16 * nrg + 15) & ~15; }
 __host__ __device__ inline int skd_off_bytes(int nrg, int nfo) { return fod_off_bytes(nrg) + 32 * nfo; }
-__host__ __device__ inline int rblock_bytes(int nrg, int nfo, int nrs) {
-    return SP_BYTES + skd_off_bytes(nrg, nfo) + 16 * nrs;
+__host__ __device__ inline int rblock_bytes(int nrg, int nfo, int nrs, int cpl) {
+    return (cpl == 2 ? Lay<2>::BYTES : Lay<1>::BYTES) + skd_off_bytes(nrg, nfo) + 16 * nrs;
 }
+template <int CPL>
 __device__ __forceinline__ RView rview(char* spbase, const DevMech& /*M*/) {
     RView r;
     r.sp = reinterpret_cast<double*>(spbase);
-    r.rxd = reinterpret_cast<double*>(spbase + SP_BYTES);
-    r.fod = reinterpret_cast<double*>(spbase + SP_BYTES + MF(fod_off));
-    r.skd = reinterpret_cast<double*>(spbase + SP_BYTES + MF(skd_off));
+    r.rxd = reinterpret_cast<double*>(spbase + Lay<CPL>::BYTES);
+    r.fod = reinterpret_cast<double*>(spbase + Lay<CPL>::BYTES + MF(fod_off));
+    r.skd = reinterpret_cast<double*>(spbase + Lay<CPL>::BYTES + MF(skd_off));
     return r;
 }
 
@@ -230,10 +242,11 @@ __device__ __forceinline__ void stage_tables(const DevMech& M, char* dst) {
 }
 
 // T-only constants (src/BatchReactor.jl:14-17: T is a per-reactor constant); g/RT scratch in accw
+template <int CPL>
 __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, const RView& R, double T, int lane) {
     const double lT = log(T);
-    double* grt = R.sp + SP_ACCW;
-    if (lane == 0) R.sp[SP_ONE] = 1.0;
+    double* grt = R.sp + Lay<CPL>::ACCW;
+    if (lane == 0) R.sp[Lay<CPL>::ONE] = 1.0;
 #pragma unroll 1
     for (int k = lane; k < MF(ng); k += WAVE) {
         const double* c = MF(nasa) + 15 * k;
@@ -317,9 +330,10 @@ __device__ __forceinline__ void falloff(const double* fo, bool troe, double kinf
 
 // third-body concentrations of the efficiency sets: mc[s] = Ctot + sum (eff-1) c over the set's
 // list (one lane per set; the list entries are read 2 at a time so the loads overlap)
+template <int CPL>
 __device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb_, double* sp, double Ctot, int lane) {
-    const Tab tb = tab_view(br_lds, M);
-    const double* conc = sp + SP_CONC;
+    const Tab tb = tab_view<CPL>(br_lds, M);
+    const double* conc = sp + Lay<CPL>::CONC;
 #pragma unroll 1
     for (int t = lane; t < MF(nset); t += WAVE) {
         const uint32_t w = tb.tbs[t];
@@ -338,19 +352,21 @@ __device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb_
             const double2 e0 = *reinterpret_cast<const double2*>(tb.tbe + 16 * i);
             s0 = fma(e0.y, conc[__double_as_longlong(e0.x) & 0xFFFF], s0);
         }
-        sp[SP_MC + t] = s0 + s1;
+        sp[Lay<CPL>::MC + t] = s0 + s1;
     }
 }
 
 // rates of progress, accumulated straight into the per-species production sums:
 // accw[k] += nu_kr q_r (gas reactions), accs[k] += nu_kr q_r (surface reactions)
+template <int CPL>
 __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, const RView& R_, double RT, int lane) {
-    const Tab tb = tab_view(br_lds, M);
-    const RView R = rview((char*)R_.sp, M);
+    typedef Lay<CPL> L;
+    const Tab tb = tab_view<CPL>(br_lds, M);
+    const RView R = rview<CPL>((char*)R_.sp, M);
     const bool xm = (MF(conv) & 2) != 0;
-    const double* conc = R.sp + SP_CONC;
-    double* accw = R.sp + SP_ACCW;
-    double* accs = R.sp + SP_ACCS;
+    const double* conc = R.sp + L::CONC;
+    double* accw = R.sp + L::ACCW;
+    double* accs = R.sp + L::ACCS;
 #pragma unroll 1
     for (int r = lane; r < MF(nrg); r += WAVE) {
         const uint4 ra = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
@@ -358,14 +374,14 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
         const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
         const uint32_t info = ra.z;
         const int tbk = gi_tb(info);
-        // branch-free mass-action products: unused slots point at conc[SP_ONE] = 1; mechanisms
+        // branch-free mass-action products: unused slots point at conc[L::ONE] = 1; mechanisms
         // with at most 3 reactants / products per reaction (MF(nu4) == 0, GRI) skip the 4th slot
         double Pf = (conc[sp8(ra.x, 0)] * conc[sp8(ra.x, 1)]) * conc[sp8(ra.x, 2)];
         double Pb = (conc[sp8(ra.y, 0)] * conc[sp8(ra.y, 1)]) * conc[sp8(ra.y, 2)];
         if (MF(nu4)) { Pf *= conc[sp8(ra.x, 3)]; Pb *= conc[sp8(ra.y, 3)]; }
         double D = k.x * Pf - k.y * Pb;
         if (tbk) {
-            const double Mc = R.sp[SP_MC + gi_tbidx(info)];
+            const double Mc = R.sp[L::MC + gi_tbidx(info)];
             if (tbk == 1) D *= Mc;
             else {
                 double fac, dfac;
@@ -389,42 +405,60 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
             for (int j = 0; j < 4; ++j) if (j < nc) s += xe[j] * conc[sp8(cs, j)];
             k *= exp(-s / RT);
         }
-        // branch-free product over up to 6 reactants (pad slots = conc[SP_ONE] = 1)
+        // branch-free product over up to 6 reactants (pad slots = conc[L::ONE] = 1)
         const double P = ((conc[sp8(rec[0], 0)] * conc[sp8(rec[0], 1)]) * (conc[sp8(rec[0], 2)] * conc[sp8(rec[0], 3)])) *
                          (conc[sp8(rec[1], 0)] * conc[sp8(rec[1], 1)]);
         scatter(accs, rec[6], rec[7], rec[8], k * P);
     }
 }
 
-// residual! (src/BatchReactor.jl:312-376) for component `lane`; returns du_lane and writes the
-// diagnosed pressure to *p_out (save_data semantics).
-__device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb_, const RView& R_, double T, double Asv,
-                                      double Asv_th, double u, int lane, double* p_out) {
-    const Tab tb = tab_view(br_lds, M);
-    const RView R = rview((char*)R_.sp, M);
-    const bool gas = lane < MF(ng);
-    const bool act = lane < MF(n);
-    const double Mk = tb.molwt[lane];
+// residual! (src/BatchReactor.jl:312-376) for the components of `lane` (lane + 64 s, s < CPL):
+// du[s]; writes the diagnosed pressure to *p_out (save_data semantics).
+template <int CPL>
+__device__ __forceinline__ void rhs(const DevMech& M, const Tab& tb_, const RView& R_, double T, double Asv,
+                                    double Asv_th, const double (&u)[CPL], int lane, double* p_out,
+                                    double (&du)[CPL]) {
+    typedef Lay<CPL> L;
+    const Tab tb = tab_view<CPL>(br_lds, M);
+    const RView R = rview<CPL>((char*)R_.sp, M);
+    const int ng = MF(ng), n = MF(n);
     // Y = u/rho, x = (Y/M)/sum(Y/M), p = rho R T / Mbar (:326-338 / :349-353) give the gas
     // concentrations c_k = p x_k / (R T) = u_k / M_k exactly; p = R T sum_k c_k
-    const double c = gas ? u / Mk : u;
-    if (act) { R.sp[SP_CONC + lane] = c; R.sp[SP_ACCW + lane] = 0.0; R.sp[SP_ACCS + lane] = 0.0; }
-    const double Ctot = wave_sum(gas ? c : 0.0);
+    double cg = 0.0, Mk[CPL];
+#pragma unroll
+    for (int s = 0; s < CPL; ++s) {
+        const int k = lane + 64 * s;
+        const bool gas = k < ng;
+        Mk[s] = tb.molwt[k];
+        const double c = gas ? u[s] / Mk[s] : u[s];
+        if (k < n) { R.sp[L::CONC + k] = c; R.sp[L::ACCW + k] = 0.0; R.sp[L::ACCS + k] = 0.0; }
+        cg += gas ? c : 0.0;
+    }
+    const double Ctot = wave_sum(cg);
     const double p = R_GAS * T * Ctot;
     if (MF(nset)) {
         wave_sync();
-        third_body_sets(M, tb, R.sp, Ctot, lane);
+        third_body_sets<CPL>(M, tb, R.sp, Ctot, lane);
     }
     wave_sync();
-    production(M, tb, R, R_GAS * T, lane);                       // :344, :355
+    production<CPL>(M, tb, R, R_GAS * T, lane);                  // :344, :355
     wave_sync();
-    const double w = act ? R.sp[SP_ACCW + lane] : 0.0;
-    const double s = act ? R.sp[SP_ACCS + lane] : 0.0;
+    double w[CPL], sf[CPL];
+#pragma unroll
+    for (int s = 0; s < CPL; ++s) {
+        const int k = lane + 64 * s;
+        w[s] = k < n ? R.sp[L::ACCW + k] : 0.0;
+        sf[s] = k < n ? R.sp[L::ACCS + k] : 0.0;
+    }
     wave_sync();
     if (lane == 0) *p_out = p;
-    if (gas) return (s * Asv + w) * Mk;                          // :345, :363-370
-    if (!act) return 0.0;
-    return s * Asv_th * tb.sigma[lane] / MF(G);                   // :367 / :370
+#pragma unroll
+    for (int s = 0; s < CPL; ++s) {
+        const int k = lane + 64 * s;
+        if (k < ng) du[s] = (sf[s] * Asv + w[s]) * Mk[s];          // :345, :363-370
+        else if (k < n) du[s] = sf[s] * Asv_th * tb.sigma[k] / MF(G);   // :367 / :370
+        else du[s] = 0.0;
+    }
 }
 
 // analytic Jacobian d(du)/du, written column by column to the per-reactor workspace
@@ -435,26 +469,34 @@ __device__ __forceinline__ double rhs(const DevMech& M, const Tab& tb_, const RV
 __device__ __forceinline__ double ld_l2(const BR_GLOBAL double* p) {
     return __hip_atomic_load((const double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+template <int CPL>
 __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const RView& R_, double T, double Asv,
-                                         double Asv_th, double u, int lane, double* Jsave_, double* jscr_) {
+                                         double Asv_th, const double (&u)[CPL], int lane, double* Jsave_,
+                                         double* jscr_) {
+    typedef Lay<CPL> L;
+    constexpr int JW = 64 * CPL;   // Jacobian column stride
     BR_GLOBAL double* Jsave = launder(Jsave_);
     BR_GLOBAL double* jscr = launder(jscr_);
-    const Tab tb = tab_view(br_lds, M);
-    const RView R = rview((char*)R_.sp, M);
-    const bool gas = lane < MF(ng);
-    const bool act = lane < MF(n);
+    const Tab tb = tab_view<CPL>(br_lds, M);
+    const RView R = rview<CPL>((char*)R_.sp, M);
     const double RT = R_GAS * T;
     const bool xm = (MF(conv) & 2) != 0;
-    const double Mk = tb.molwt[lane];
-    double* conc = R.sp + SP_CONC;
-    double* accw = R.sp + SP_ACCW;
-    double* accs = R.sp + SP_ACCS;
-    const double c = gas ? u / Mk : u;                           // c_k = u_k/M_k = p x_k/(RT)
-    if (act) conc[lane] = c;
-    const double Ctot = wave_sum(gas ? c : 0.0);
+    double* conc = R.sp + L::CONC;
+    double* accw = R.sp + L::ACCW;
+    double* accs = R.sp + L::ACCS;
+    double cg = 0.0;
+#pragma unroll
+    for (int s = 0; s < CPL; ++s) {
+        const int k = lane + 64 * s;
+        const bool gas = k < MF(ng);
+        const double c = gas ? u[s] / tb.molwt[k] : u[s];          // c_k = u_k/M_k = p x_k/(RT)
+        if (k < MF(n)) conc[k] = c;
+        cg += gas ? c : 0.0;
+    }
+    const double Ctot = wave_sum(cg);
     wave_sync();
     if (MF(nset)) {
-        third_body_sets(M, tb, R.sp, Ctot, lane);
+        third_body_sets<CPL>(M, tb, R.sp, Ctot, lane);
         wave_sync();
     }
 #pragma unroll 1
@@ -469,7 +511,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
         const double D = kf * Pf - kr * Pb;
         double pre = 1.0, coefM = 0.0;
         if (tbk) {
-            const double Mc = R.sp[SP_MC + gi_tbidx(info)];
+            const double Mc = R.sp[L::MC + gi_tbidx(info)];
             if (tbk == 1) { pre = Mc; coefM = 1.0; }
             else {
                 double fac, dfac;
@@ -497,7 +539,11 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
     wave_sync();
 #pragma unroll 1
     for (int j = 0; j < MF(n); ++j) {
-        if (act) { accw[lane] = 0.0; accs[lane] = 0.0; }
+#pragma unroll
+        for (int s = 0; s < CPL; ++s) {
+            const int k = lane + 64 * s;
+            if (k < MF(n)) { accw[k] = 0.0; accs[k] = 0.0; }
+        }
         wave_sync();
         const int cb = MF(col_ptr)[j], ce = MF(col_ptr)[j + 1];
 #pragma unroll 1
@@ -566,12 +612,18 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
             }
         }
         wave_sync();
-        const double w = act ? accw[lane] : 0.0;
-        const double s = act ? accs[lane] : 0.0;
-        double v;
-        if (gas) v = (j < MF(ng) ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * s;
-        else v = Asv_th * tb.sigma[lane] / MF(G) * s;
-        Jsave[j * WAVE + lane] = act ? v : 0.0;
+#pragma unroll
+        for (int s = 0; s < CPL; ++s) {
+            const int k = lane + 64 * s;
+            const bool act = k < MF(n);
+            const double w = act ? accw[k] : 0.0;
+            const double sf = act ? accs[k] : 0.0;
+            const double Mk = tb.molwt[k];
+            double v;
+            if (k < MF(ng)) v = (j < MF(ng) ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * sf;
+            else v = Asv_th * tb.sigma[k] / MF(G) * sf;
+            Jsave[j * JW + k] = act ? v : 0.0;
+        }
         wave_sync();
     }
 }
@@ -808,6 +860,249 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
     r *= wsg[NMAX * WAVE + lane];                  // D^-1
     r = tri_sweep<false, NCH>(wsg, lane, n, r);    // backward, unit upper
     return (lane < n) ? r : 0.0;
+}
+
+// ------------------------------------------------------------------------------------
+// 64 < n <= 128 (CPL = 2): lane holds rows lane and lane + 64. Same factorization semantics
+// (first max |a_ik| in row order, same multipliers and update order); column stride 128; the
+// panels are 16 columns wide (registers: 2 x 16 per lane); the inverse permutation and the
+// row gathers of P b and D^-1 go through LDS scratch (>= 192 doubles) instead of ds_permute.
+// ------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) double LDSd;
+typedef __attribute__((address_space(3))) int LDSi;
+
+__device__ __forceinline__ int pivot_row2(double v0, bool c0, double v1, bool c1) {
+    const unsigned long long b0 = (unsigned long long)__double_as_longlong(v0);
+    const unsigned long long b1 = (unsigned long long)__double_as_longlong(v1);
+    const unsigned h0 = c0 ? (unsigned)(b0 >> 32) : 0u, h1 = c1 ? (unsigned)(b1 >> 32) : 0u;
+    const unsigned mh = wave_umax(max(h0, h1));
+    const bool t0 = c0 && h0 == mh, t1 = c1 && h1 == mh;
+    unsigned long long m0 = __ballot(t0), m1 = __ballot(t1);
+    if (__builtin_popcountll(m0) + __builtin_popcountll(m1) > 1) {
+        const unsigned l0 = t0 ? (unsigned)b0 : 0u, l1 = t1 ? (unsigned)b1 : 0u;
+        const unsigned ml = wave_umax(max(l0, l1));
+        m0 = __ballot(t0 && l0 == ml);
+        m1 = __ballot(t1 && l1 == ml);
+    }
+    return m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : 0);
+}
+
+template <int W>
+__device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, int cend, int lane, int (&pstep)[2],
+                                             double (&dinv)[2], int& fail, const LUWs& F) {
+    constexpr int CH = 8, JW = 128;
+    static_assert(W % CH == 0, "W must be a multiple of 8");
+#pragma unroll 1
+    for (int k = k0; k < k1; ++k) {
+        const int pr = pivot_row2(fabs(a[0][0]), pstep[0] < 0, fabs(a[1][0]), pstep[1] < 0);
+        const int p = pr & 63, ps = pr >> 6;
+        const double piv = ps ? bcast(a[1][0], p) : bcast(a[0][0], p);
+        if (piv == 0.0 && !fail) fail = k + 1;
+        const double rinv = 1.0 / piv;
+        double l[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const bool isp = (ps == s) && (lane == p);
+            const bool rem = (pstep[s] < 0) && !isp;
+            l[s] = rem ? a[s][0] * rinv : 0.0;
+            F.M[k * JW + 64 * s + lane] = rem ? l[s] : ((pstep[s] >= 0) ? a[s][0] * dinv[s] : 0.0);
+            if (isp) { pstep[s] = k; dinv[s] = rinv; }
+        }
+        const int live = cend - k;
+        auto upd = [&](auto S) {
+            constexpr int src = decltype(S)::value;
+#pragma unroll
+            for (int c = 0; c < W; c += CH) {
+                if (c < live) {
+#pragma unroll
+                    for (int i = 0; i < CH; ++i) {
+                        const int j = c + i;
+                        if (j + 1 < W) {
+                            const double u = bcast(a[src][j + 1], p);
+                            a[0][j] = fma(-u, l[0], a[0][j + 1]);
+                            a[1][j] = fma(-u, l[1], a[1][j + 1]);
+                        } else {
+                            a[0][j] = 0.0;
+                            a[1][j] = 0.0;
+                        }
+                    }
+                }
+            }
+        };
+        if (ps) upd(std::integral_constant<int, 1>{});
+        else upd(std::integral_constant<int, 0>{});
+    }
+}
+
+// one 16-column panel starting at column C0: load, left-looking updates by steps 0..C0-1
+// (multipliers from M in original row order, masked to rows not yet pivoted at that step),
+// right-looking factorization of its own columns; then the next panel
+template <int NMAX, int C0>
+__device__ __forceinline__ void lu2_panels(const BR_GLOBAL double* J, double gamma, int n, int lane, int (&pstep)[2],
+                                           double (&dinv)[2], int& fail, const LUWs& F) {
+    if constexpr (C0 < NMAX) {
+        constexpr int JW = 128, W = (NMAX - C0) < 16 ? (NMAX - C0) : 16;
+        if (C0 < n) {
+            double a[2][W];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int row = lane + 64 * s;
+#pragma unroll
+                for (int j = 0; j < W; ++j) {
+                    const int col = C0 + j;
+                    const double jv = (col < n && row < n) ? J[col * JW + row] : 0.0;
+                    a[s][j] = ((col == row) ? 1.0 : 0.0) - gamma * jv;
+                }
+            }
+            if (C0 > 0) {
+                double n0 = F.M[lane], n1 = F.M[64 + lane];
+#pragma unroll 1
+                for (int k = 0; k < C0; ++k) {
+                    const double m0 = n0, m1 = n1;
+                    const int kn = (k + 1 < C0) ? k + 1 : k;
+                    n0 = F.M[kn * JW + lane];
+                    n1 = F.M[kn * JW + 64 + lane];
+                    const unsigned long long b0 = __ballot(pstep[0] == k), b1 = __ballot(pstep[1] == k);
+                    const int p = b0 ? (int)__builtin_ctzll(b0) : (int)__builtin_ctzll(b1);
+                    const double l0 = ((unsigned)pstep[0] > (unsigned)k) ? m0 : 0.0;
+                    const double l1 = ((unsigned)pstep[1] > (unsigned)k) ? m1 : 0.0;
+                    auto upd = [&](auto S) {
+                        constexpr int src = decltype(S)::value;
+#pragma unroll
+                        for (int j = 0; j < W; ++j) {
+                            const double u = bcast(a[src][j], p);
+                            a[0][j] = fma(-u, l0, a[0][j]);
+                            a[1][j] = fma(-u, l1, a[1][j]);
+                        }
+                    };
+                    if (b0) upd(std::integral_constant<int, 0>{});
+                    else upd(std::integral_constant<int, 1>{});
+                }
+            }
+            const int kend = (C0 + W < n) ? C0 + W : n;
+            lu_rl_steps2<W>(a, C0, kend, kend, lane, pstep, dinv, fail, F);
+        }
+        lu2_panels<NMAX, C0 + 16>(J, gamma, n, lane, pstep, dinv, fail, F);
+    }
+}
+
+template <int NMAX>
+__device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double* __restrict__ ws, LDSd* scr,
+                                          double gamma, int n, int lane, int (&perm_out)[2]) {
+    constexpr int JW = 128, CH = 4, NC = NMAX / CH;
+    static_assert(NMAX % 8 == 0 && NMAX <= 128, "NMAX");
+    const BR_GLOBAL double* J = launder(J_);
+    BR_GLOBAL double* wsg = launder(ws);
+    const LUWs F{wsg, wsg + NMAX * JW};
+    lane = launder_v(lane);
+    int pstep[2];
+    double dinv[2] = {0.0, 0.0};
+    int fail = 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) pstep[s] = (lane + 64 * s < n) ? -1 : 1024;
+    lu2_panels<NMAX, 0>(J, gamma, n, lane, pstep, dinv, fail, F);
+    // inverse permutation through LDS: step s <- row perm[s] (rows >= n map to themselves)
+    LDSi* isc = (LDSi*)scr;
+    LDSd* dsc = scr + 64;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int row = lane + 64 * s;
+        isc[(row < n) ? pstep[s] : row] = row;
+        dsc[row] = dinv[s];
+    }
+    wave_sync();
+    int perm[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        perm[s] = isc[lane + 64 * s];
+        F.D[64 * s + lane] = dsc[perm[s]];
+    }
+    wave_sync();
+    // rows into step order, in place, chunks of CH columns double-buffered (columns >= n: zeros)
+    double g[2][2][CH];
+    auto gather = [&](double (&v)[2][CH], int c) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int col = (c + i < n) ? c + i : n - 1;
+            v[0][i] = F.M[col * JW + perm[0]];
+            v[1][i] = F.M[col * JW + perm[1]];
+        }
+    };
+    gather(g[0], 0);
+#pragma unroll
+    for (int t = 0; t < NC; ++t) {
+        if (t + 1 < NC) gather(g[(t + 1) & 1], (t + 1) * CH);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int col = t * CH + i;
+            F.M[col * JW + lane] = (col < n) ? g[t & 1][0][i] : 0.0;
+            F.M[col * JW + 64 + lane] = (col < n) ? g[t & 1][1][i] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    perm_out[0] = perm[0];
+    perm_out[1] = perm[1];
+    return fail;
+}
+
+// forward / backward sweeps over the step-ordered 128-row columns (fully unrolled: the column
+// of every FMA, and so the lane and row set holding r[k], are compile-time constants)
+template <bool FWD, int NMAX>
+__device__ __forceinline__ void tri_sweep2(const BR_GLOBAL double* __restrict__ col, int lane, int n, double (&r)[2]) {
+    constexpr int JW = 128, NCH = NMAX / 8;
+    double v[2][2][8];
+    const int row0 = min(lane, n - 1), row1 = min(lane + 64, n - 1);
+    auto load = [&](double (&b)[2][8], int c) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            b[0][i] = col[(c + i) * JW + row0];
+            b[1][i] = col[(c + i) * JW + row1];
+        }
+    };
+    auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
+    load(v[0], cidx(0));
+    if (NCH > 1) load(v[1], cidx(1));
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int c = cidx(t);
+#pragma unroll
+        for (int ii = 0; ii < 8; ++ii) {
+            const int i = FWD ? ii : 7 - ii;
+            const int k = c + i;
+            const double x = bcast(r[k >> 6], k & 63);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int row = lane + 64 * s;
+                const bool upd = FWD ? (row > k && row < n) : (row < k && k < n);
+                const double tt = fma(-v[t & 1][s][i], x, r[s]);
+                r[s] = upd ? tt : r[s];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < NCH) load(v[t & 1], cidx(t + 2));
+    }
+}
+
+template <int NMAX>
+__device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* scr, int n, int lane,
+                                          const int (&perm)[2], double (&b)[2]) {
+    constexpr int JW = 128;
+    const BR_GLOBAL double* wsg = launder(ws);
+    lane = launder_v(lane);
+    LDSd* dsc = scr + 64;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) dsc[lane + 64 * s] = (lane + 64 * s < n) ? b[s] : 0.0;
+    wave_sync();
+    double r[2] = {dsc[perm[0]], dsc[perm[1]]};   // P b
+    wave_sync();
+    tri_sweep2<true, NMAX>(wsg, lane, n, r);
+    r[0] *= wsg[NMAX * JW + lane];
+    r[1] *= wsg[NMAX * JW + 64 + lane];
+    tri_sweep2<false, NMAX>(wsg, lane, n, r);
+    b[0] = (lane < n) ? r[0] : 0.0;
+    b[1] = (lane + 64 < n) ? r[1] : 0.0;
 }
 
 }  // namespace brhip

@@ -51,7 +51,7 @@ class Engine:
         _lib.check(L.br_mech_create(C.byref(desc), device, C.byref(h)))
         self.h = h
         self.n, self.ng, self.ns = mech.n, mech.ng, mech.ns
-        self.nmax = 16 if self.n <= 16 else 32 if self.n <= 32 else 56 if self.n <= 56 else 64   # kernel tile
+        self.nmax = 16 if self.n <= 16 else 32 if self.n <= 32 else 56 if self.n <= 56 else 64 if self.n <= 64 else 72   # kernel tile
 
     def close(self):
         if getattr(self, "h", None):
@@ -97,7 +97,8 @@ class Engine:
 
     def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000, trace_cap=0):
         """Integrate N reactors 0 -> tf. With trace_cap > 0 also returns the per-step rows
-        trace[N, trace_cap+1, n+4] = (t, h, q, p_last, u...)."""
+        trace[N, trace_cap+1, 2n+4] = (t, h, q, p_last, u[n], y_last[n]): u the accepted state, y_last
+        and p_last the state and pressure of the step's last RHS evaluation (save_data semantics)."""
         u = np.array(np.atleast_2d(u0), dtype=np.float64, order="C")
         N = u.shape[0]
         T, A, tf = self._arr(T, N), self._arr(Asv, N), self._arr(tf, N)
@@ -105,7 +106,7 @@ class Engine:
         o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0, trace_cap)
         L = _lib.lib()
         if trace_cap > 0:
-            tr = np.zeros((N, trace_cap + 1, self.n + 4))
+            tr = np.zeros((N, trace_cap + 1, 2 * self.n + 4))
             _lib.check(L.br_integrate_traced(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(tf),
                                              C.byref(o), _lib.dptr(st), _lib.dptr(tr)))
         else:

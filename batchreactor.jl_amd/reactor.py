@@ -97,16 +97,23 @@ def batch_reactor(input_file, lib_dir, udf=None, *, sens=False, surfchem=False, 
     if sens:
         return (dict(mech=mech, T=T, Asv=Asv, chem=chem), u0, (0.0, tf))
     eng = _engine(mech, device)
-    u, st = eng.integrate([T], [Asv], u0[None, :], [tf])
+    # one row per accepted step (save_data callback, :383-402): rho from the accepted state u,
+    # x, p and coverages from the step's last RHS evaluation (the engine's trace rows carry both)
+    cap = 4096
+    while True:
+        u, st, tr = eng.integrate([T], [Asv], u0[None, :], [tf], trace_cap=cap)
+        nst = int(st["nsteps"][0])
+        if nst < cap:
+            break
+        cap = 2 * nst
+    n, ng = mech.n, mech.ng
     folder = os.path.dirname(os.path.abspath(input_file))
     streams = _write_headers(folder, mech, surfchem)
     try:
-        _row(streams, mech, surfchem, 0.0, T, p0, u0[:mech.ng].sum(), x, u0[mech.ng:])
-        uf = u[0]
-        xf = mech.state_to_molefrac(uf)
-        rho = uf[:mech.ng].sum()
-        pf = rho * R_GAS * T / float(np.sum(xf * mech.molwt))
-        _row(streams, mech, surfchem, tf, T, pf, rho, xf, uf[mech.ng:])
+        for k in range(nst + 1):
+            row = tr[0, k]
+            uk, yk = row[4:4 + n], row[4 + n:4 + 2 * n]
+            _row(streams, mech, surfchem, row[0], T, row[3], uk[:ng].sum(), mech.state_to_molefrac(yk), yk[ng:])
     finally:
         for s in streams:
             s.close()

@@ -118,9 +118,11 @@ int br_integrate(br_mech* m, int N, const double* T, const double* Asv, double* 
                  const double* tf, const br_opts* opts, br_stats* stats /*[N] or NULL*/);
 
 /* as br_integrate, and also records the state after every accepted step (the rows
- * save_data writes, src/BatchReactor.jl:383-402): trace[N][trace_cap+1][n+4] with
- * row = (t, h, q, p_last, u[0..n-1]); row 0 is t=0; unused rows are left as zeros.
- * The last written row is the tstop row (t = tf). */
+ * save_data writes, src/BatchReactor.jl:383-402): trace[N][trace_cap+1][2n+4] with
+ * row = (t, h, q, p_last, u[0..n-1], y[0..n-1]): u is the accepted state, y and p_last the state
+ * and pressure of the last RHS evaluation of that step (save_data reads x, p and coverages from
+ * the last RHS call and rho from u). Row 0 is t=0; unused rows are left as zeros. The last
+ * written row is the tstop row (t = tf). */
 int br_integrate_traced(br_mech* m, int N, const double* T, const double* Asv, double* u,
                         const double* tf, const br_opts* opts, br_stats* stats, double* trace);
 

@@ -33,6 +33,7 @@ CASES = {
     "h2o2": dict(gas="h2o2.dat", surf=None),
     "gri": dict(gas="grimech.dat", surf=None),
     "surf": dict(gas=None, surf="ch4ni.xml"),
+    "gas_surf": dict(gas="grimech.dat", surf="ch4ni.xml"),   # n = 66: two components per lane
 }
 
 
@@ -74,7 +75,7 @@ def _scale(pm, qg, qs):
     return sc
 
 
-@pytest.mark.parametrize("case", ["h2o2", "gri", "surf"])
+@pytest.mark.parametrize("case", ["h2o2", "gri", "surf", "gas_surf"])
 def test_rates_parity(pkg, orc, gpu, case):
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
@@ -90,7 +91,7 @@ def test_rates_parity(pkg, orc, gpu, case):
             assert np.all(np.abs(s[i] - so) <= 1e-12 * sc + 1e-300), (case, i)
 
 
-@pytest.mark.parametrize("case", ["h2o2", "gri", "surf"])
+@pytest.mark.parametrize("case", ["h2o2", "gri", "surf", "gas_surf"])
 def test_rhs_and_jacobian_parity(pkg, orc, gpu, case):
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
@@ -151,7 +152,7 @@ def _global_err(X, Ut):
     return e.max(axis=1)
 
 
-@pytest.mark.parametrize("case,N", [("h2o2", 256), ("gri", 64), ("surf", 64)])
+@pytest.mark.parametrize("case,N", [("h2o2", 256), ("gri", 64), ("surf", 64), ("gas_surf", 32)])
 def test_integrate_parity(pkg, orc, gpu, case, N):
     """Default tolerances (rtol 1e-6, atol 1e-10, src/BatchReactor.jl:141,:210), 0 -> 10 s through
     ignition, on a slice of the synthetic ensemble (bench inputs).
@@ -176,7 +177,9 @@ def test_integrate_parity(pkg, orc, gpu, case, N):
     sg = st["status"]
     sa = np.array([s["status"] for s in sta])
     sd = np.array([s["status"] for s in std_])
-    assert set(np.unique(sg)) <= {0, -7}                     # success or runaway stop, nothing else
+    # success, runaway stop, or (gas+surface: ~0.5 % of reactors, oracle alike) repeated error-test
+    # failures; the failure fraction must match the oracle's
+    assert set(np.unique(sg)) <= ({0, -7, -3} if case == "gas_surf" else {0, -7})
     assert abs(np.mean(sg != 0) - np.mean(sa != 0)) <= 0.03 + 2.0 / N
     ok = (sg == 0) & (sa == 0) & (sd == 0) & np.array([s["status"] == 0 for s in stt])
     assert ok.sum() >= 0.9 * N
@@ -191,7 +194,7 @@ def test_integrate_parity(pkg, orc, gpu, case, N):
     assert abs(ng_ - no_) <= 0.1 * no_, (ng_, no_)
 
 
-@pytest.mark.parametrize("case,N", [("h2o2", 16), ("gri", 4), ("surf", 8)])
+@pytest.mark.parametrize("case,N", [("h2o2", 16), ("gri", 4), ("surf", 8), ("gas_surf", 2)])
 def test_integrate_parity_tight(pkg, orc, gpu, case, N):
     """Tight tolerances (rtol 1e-10, atol 1e-16) on both sides: the two integrations converge to the
     same trajectory, so the end states (tf = 1e-2 s, through ignition for the gas cases) must agree
@@ -243,7 +246,7 @@ def test_programmatic_api(pkg, gpu):
     assert t[-1] == 10.0 and abs(sum(xd.values()) - 1) < 1e-12
 
 
-@pytest.mark.parametrize("n", [9, 20, 53])
+@pytest.mark.parametrize("n", [9, 20, 53, 66, 72])
 def test_batched_lu_solve(pkg, gpu, n):
     """The integrator's row-per-lane LU (partial pivoting, no row swaps) + solve against numpy on
     random, ill-scaled Newton matrices I - gamma J (fp64; 1e-12 backward-error bound)."""
@@ -263,3 +266,85 @@ def test_batched_lu_solve(pkg, gpu, n):
         A = np.eye(n) - g[i] * J[i]
         res = A @ x[i] - b[i]
         assert np.max(np.abs(res)) <= 1e-12 * (np.abs(A).sum(1).max() * np.abs(x[i]).max() + np.abs(b[i]).max())
+
+
+def test_gas_surf_golden_early_steps(pkg, gpu):
+    """The reference's own gas+surface output (test/batch_gas_and_surf, GRI + ch4ni, T = 1173 K,
+    Asv = 1, rtol 1e-6 / atol 1e-10; tests/golden/gas_and_surf_*golden.csv) against the engine's
+    per-step trace of the same run (n = 66, two components per lane): the first 11 accepted step
+    times to 1e-4, coverages above 1e-12 and the surface-driven gas species to 1e-4 relative, and
+    the pressure of the last RHS evaluation (save_data semantics, src/BatchReactor.jl:383-402)."""
+    import csv
+    from conftest import GOLDEN
+
+    def golden(name):
+        rows = list(csv.reader(open(os.path.join(GOLDEN, name))))
+        return np.array([[float(v) for v in r[1:]] for r in rows[1:]]), [int(r[0]) for r in rows[1:]]
+
+    g, idx = golden("gas_and_surf_golden.csv")
+    s, _ = golden("gas_and_surf_covg_golden.csv")
+    assert idx[:12] == list(range(12))
+    pm = pkg.Mechanism.from_files(LIB, gas_mech="grimech.dat", surface_mech="ch4ni.xml")
+    assert pm.n == 66
+    x = pm.mole_fractions({"CH4": 0.25, "O2": 0.5, "N2": 0.25})
+    u0 = pm.initial_state(1173.0, 1e5, x)
+    eng = pkg.Engine(pm)
+    U, st, tr = eng.integrate(np.array([1173.0]), np.array([1.0]), u0[None, :], 10.0, trace_cap=12, max_steps=12)
+    rows = tr[0]
+    M = np.asarray(pm.molwt)
+    n = pm.n
+    for i in range(1, 12):
+        t, p, u = rows[i, 0], rows[i, 3], rows[i, 4 + n:4 + 2 * n]    # last-RHS state (save_data)
+        assert abs(t / g[i, 0] - 1) < 1e-4, (i, t, g[i, 0])
+        th = u[pm.ng:]
+        gth = s[i, 2:]
+        big = gth > 1e-12
+        assert np.max(np.abs(th[big] / gth[big] - 1)) < 1e-4, (i, t)
+        xm = (u[:pm.ng] / M) / np.sum(u[:pm.ng] / M)
+        for name in ("H2O", "CH4", "O2", "N2"):
+            k = pm.gas_species.index(name)
+            assert abs(xm[k] / g[i, 4 + k] - 1) < 1e-4, (i, name)
+        assert abs(p / g[i, 2] - 1) < 1e-9, (i, p, g[i, 2])
+        assert abs(rows[i, 4:4 + pm.ng].sum() / g[i, 3] - 1) < 1e-6, i       # rho from the accepted u
+
+
+def test_file_driven_gas_surf_profiles(pkg, gpu, tmp_path):
+    """batch_reactor(input_file, lib_dir; surfchem, gaschem) on test/batch_gas_and_surf (the
+    reference's testset "Batch gas and surface chemistry", test/runtests.jl): returns "Success" and
+    writes gas_profile / surface_covg .dat + .csv with one row per accepted step (save_data,
+    src/BatchReactor.jl:383-402). Against the reference's own CSVs: same headers, the same first
+    11 rows (step times, p, rho, surface-driven species, coverages), the final row at t = 10 s and
+    a step count within 15 % of the reference's 1918."""
+    import csv
+    import shutil
+    from conftest import GOLDEN
+    d = tmp_path / "batch_gas_and_surf"
+    d.mkdir()
+    shutil.copy(os.path.join(GOLDEN, "batch_gas_and_surf", "batch.xml"), d / "batch.xml")
+    ret = pkg.batch_reactor(str(d / "batch.xml"), LIB, surfchem=True, gaschem=True)
+    assert ret == "Success"
+    gas = list(csv.reader(open(d / "gas_profile.csv")))
+    cov = list(csv.reader(open(d / "surface_covg.csv")))
+    ref = list(csv.reader(open(os.path.join(GOLDEN, "gas_and_surf_golden.csv"))))
+    refc = list(csv.reader(open(os.path.join(GOLDEN, "gas_and_surf_covg_golden.csv"))))
+    assert gas[0] == ref[0][1:] and cov[0] == refc[0][1:]          # fixture rows carry a row index
+    assert abs(len(gas) - 1 - 1918) <= 0.15 * 1918 and len(cov) == len(gas)
+    assert float(gas[-1][0]) == 10.0
+    hdr = gas[0]
+
+    def rel(a, b, tol):
+        return abs(a - b) <= tol * abs(b)
+
+    for i in range(1, 13):                                           # CSV rows 1..12 = steps 0..11
+        g = np.array([float(v) for v in gas[i]])
+        r = np.array([float(v) for v in ref[i][1:]])
+        assert rel(g[0], r[0], 1e-4) and rel(g[2], r[2], 1e-9) and rel(g[3], r[3], 1e-6), (i, g[:4], r[:4])
+        for name in ("H2O", "CH4", "O2", "N2"):
+            k = hdr.index(name)
+            assert rel(g[k], r[k], 1e-4), (i, name)
+        c = np.array([float(v) for v in cov[i]])[2:]
+        rc = np.array([float(v) for v in refc[i][1:]])[2:]
+        big = rc > 1e-12
+        assert np.max(np.abs(c[big] / rc[big] - 1)) < 1e-4, i
+    dat = open(d / "gas_profile.dat").read().splitlines()
+    assert len(dat) == len(gas) and dat[0].split() == hdr
