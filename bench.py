@@ -26,6 +26,8 @@ CONFIGS = {
                 name="C3 test/batch_ch4 GRI-Mech 3.0 CH4/O2/N2 ensemble (53 species, 325 reactions)"),
     "h2o2": dict(gas="h2o2.dat", surf=None, n=1000000, tf=10.0, name="C2 H2/O2 ignition ensemble (9 species)"),
     "surf": dict(gas=None, surf="ch4ni.xml", n=100000, tf=10.0, name="C4 surface-only Ni/CH4 ensemble"),
+    "gas_surf": dict(gas="grimech.dat", surf="ch4ni.xml", n=100000, tf=10.0,
+                     name="C5 GRI-Mech 3.0 gas + Ni surface ensemble (66 components, 325+42 reactions)"),
 }
 
 
@@ -55,14 +57,15 @@ def main():
     dev = torch.device("cuda", local)
 
     pkg = _pkgload.load()
-    from batchreactor_amd import ensemble
+    from batchreactor_amd import ensemble, shard
     cfg = CONFIGS[args.config]
     lib = os.path.join(ROOT, "tests", "golden", "lib")
     mech = pkg.Mechanism.from_files(lib, gas_mech=cfg["gas"], surface_mech=cfg["surf"],
                                     gasphase=None if cfg["gas"] else "CH4 H2O H2 CO CO2 O2 N2".split())
     eng = pkg.Engine(mech, device=local)
     N = args.n or cfg["n"]
-    T, Asv, U0 = ensemble.make_inputs(mech, args.config, rank * N, N)
+    start, _ = shard.shard_slice(rank, N)
+    T, Asv, U0 = ensemble.make_inputs(mech, args.config, start, N)
     tf = np.full(N, cfg["tf"])
     dT = torch.from_numpy(T).to(dev)
     dA = torch.from_numpy(Asv).to(dev)
@@ -92,11 +95,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    elapsed = float(tt.item())
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None, dev)
 
     st = dst.cpu().numpy()
     stats = {k: st[:, i] for i, k in enumerate(pkg.STAT_FIELDS)}
@@ -114,11 +113,9 @@ def main():
 
     gather_ms = None
     if world > 1:   # the single result gather over RCCL/xGMI (outside the timed region)
-        payload = torch.cat([dU, dst], dim=1).contiguous()
-        out = torch.empty((world * N, payload.shape[1]), dtype=payload.dtype, device=dev)
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        dist.all_gather_into_tensor(out, payload)
+        shard.gather_ensemble(dU, dst, dist)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
 

@@ -1,0 +1,72 @@
+"""The multi-GPU path on CPU: two ranks over gloo run exactly the code bench.py runs over RCCL
+(batchreactor.jl_amd/shard.py: contiguous per-rank slices of the ensemble, no collective during
+the integration, one all-gather of final states + counters, max-over-ranks time). The per-rank
+compute is the CPU oracle here (no GPU); the gathered ensemble must equal a single-process run
+over the whole range, in order.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PER_RANK = 3
+TF = 2e-3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _inputs(pkg, start, count):
+    from batchreactor_amd import ensemble
+    m = pkg.Mechanism.from_files(os.path.join(ROOT, "tests", "golden", "lib"), gas_mech="h2o2.dat")
+    return m, ensemble.make_inputs(m, "h2o2", start, count)
+
+
+def _oracle_run(m, T, Asv, U0):
+    import oracle
+    lib = os.path.join(ROOT, "tests", "golden", "lib")
+    om = oracle.Mech(os.path.join(lib, "h2o2.dat"), os.path.join(lib, "therm.dat"))
+    U, st, _ = om.integrate_batch(T, Asv, U0, np.full(len(T), TF), analytic_jac=True, nthreads=1)
+    S = np.array([[s["nsteps"], s["nfe"], s["status"]] for s in st], dtype=np.float64)
+    return U, S
+
+
+def _rank(rank, world, port, out_dir):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+    import _pkgload
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = _pkgload.load()
+    from batchreactor_amd import shard
+    start, stop = shard.shard_slice(rank, PER_RANK)
+    m, (T, Asv, U0) = _inputs(pkg, start, stop - start)
+    U, S = _oracle_run(m, T, Asv, U0)
+    t = shard.max_over_ranks(0.5 + rank, dist)
+    Ug, Sg = shard.gather_ensemble(torch.from_numpy(U), torch.from_numpy(S), dist)
+    np.save(os.path.join(out_dir, f"U{rank}.npy"), Ug.numpy())
+    np.save(os.path.join(out_dir, f"S{rank}.npy"), Sg.numpy())
+    np.save(os.path.join(out_dir, f"t{rank}.npy"), np.array([t]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shard_and_gather(pkg, orc, tmp_path):
+    world = 2
+    mp.start_processes(_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    m, (T, Asv, U0) = _inputs(pkg, 0, world * PER_RANK)
+    U, S = _oracle_run(m, T, Asv, U0)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"U{r}.npy"), U)   # same inputs, same order
+        np.testing.assert_array_equal(np.load(tmp_path / f"S{r}.npy"), S)
+        assert float(np.load(tmp_path / f"t{r}.npy")[0]) == 0.5 + (world - 1)
