@@ -367,10 +367,8 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
     const double* conc = R.sp + L::CONC;
     double* accw = R.sp + L::ACCW;
     double* accs = R.sp + L::ACCS;
-#pragma unroll 1
-    for (int r = lane; r < MF(nrg); r += WAVE) {
-        const uint4 ra = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
-        const uint4 rb = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
+    // net rate of progress of gas reaction r (mass action x third body / falloff)
+    auto rate = [&](int r, const uint4& ra) -> double {
         const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
         const uint32_t info = ra.z;
         const int tbk = gi_tb(info);
@@ -390,7 +388,23 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
                 if (xm) D *= Mc;
             }
         }
-        scatter(accw, rb.x, rb.y, rb.z, D);
+        return D;
+    };
+    // two reactions per lane and iteration (r and r + 64): their LDS gather chains overlap
+    const int nrg = MF(nrg);
+#pragma unroll 1
+    for (int r = lane; r < nrg; r += 2 * WAVE) {
+        const int r1 = r + WAVE;
+        const bool has1 = r1 < nrg;
+        const int q1 = has1 ? r1 : r;
+        const uint4 ra0 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
+        const uint4 rb0 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
+        const uint4 ra1 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * q1);
+        const uint4 rb1 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * q1 + 4);
+        const double D0 = rate(r, ra0);
+        const double D1 = rate(q1, ra1);
+        scatter(accw, rb0.x, rb0.y, rb0.z, D0);
+        if (has1) scatter(accw, rb1.x, rb1.y, rb1.z, D1);
     }
 #pragma unroll 1
     for (int r = lane; r < MF(nrs); r += WAVE) {
