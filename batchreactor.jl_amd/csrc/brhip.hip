@@ -160,19 +160,36 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
     double tau[QMAX + 2];
 #pragma unroll
     for (int i = 0; i < QMAX + 2; ++i) tau[i] = ud(C->tau[i]);
-    double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = h;
-    if (q > 1) {
-        for (int j = 2; j < q; ++j) {
-            hsum += tau[j - 1];
-            xi_inv = h / hsum;
-            alpha0 -= inv_int(j);
+    // h / hsum_m for every m up front (hsum_m = h + tau[1] + ... + tau[m-1], summed in CVODE's
+    // order): the divisions are independent, so they overlap instead of forming a chain
+    double xinv[QMAX + 2];
+    {
+        double hs = h;
 #pragma unroll
-            for (int i = QMAX; i >= 1; --i) if (i <= j) lv[i] += lv[i - 1] * xi_inv;
+        for (int m = 2; m <= QMAX + 1; ++m) {
+            hs += tau[m - 1];
+            xinv[m] = h / hs;
+        }
+    }
+    auto xinv_at = [&](int m) {   // uniform m in [2, QMAX + 1]
+        double v = xinv[2];
+#pragma unroll
+        for (int i = 3; i <= QMAX + 1; ++i) v = (m == i) ? xinv[i] : v;
+        return v;
+    };
+    double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0;
+    if (q > 1) {
+#pragma unroll
+        for (int j = 2; j < QMAX; ++j) {
+            if (j < q) {
+                alpha0 -= inv_int(j);
+#pragma unroll
+                for (int i = QMAX; i >= 1; --i) if (i <= j) lv[i] += lv[i - 1] * xinv[j];
+            }
         }
         alpha0 -= inv_int(q);
         xistar_inv = -lv[1] - alpha0;
-        hsum += tau[q - 1];
-        xi_inv = h / hsum;
+        xi_inv = xinv_at(q);
         alpha0_hat = -lv[1] - xi_inv;
 #pragma unroll
         for (int i = QMAX; i >= 1; --i) if (i <= q) lv[i] += lv[i - 1] * xistar_inv;
@@ -193,8 +210,7 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
             const double Cpinv = (1.0 - A4 + A3) / A3;
             C->tq[1] = fabs(Cc * Cpinv);
         } else C->tq[1] = 1.0;
-        hsum += tau[q];
-        xi_inv = h / hsum;
+        xi_inv = xinv_at(q + 1);   // h / (h + tau[1] + ... + tau[q])
         const double A5 = alpha0 - inv_int(q + 1);
         const double A6 = alpha0_hat - xi_inv;
         const double Cppinv = (1.0 - A6 + A5) / A2;
