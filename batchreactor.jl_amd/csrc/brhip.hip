@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -745,6 +746,8 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (
     return A_RHS;
 }
 
+#include "brhip_lane.hpp"   // one reactor per lane (small gas mechanisms)
+
 // ------------------------------------------------------------------------------------
 // the integrator kernel: one reactor per 64-lane wavefront, `rpb` reactors per workgroup
 // ------------------------------------------------------------------------------------
@@ -1001,6 +1004,12 @@ struct br_mech {
     size_t jws_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
+    // one-reactor-per-lane engine (brhip_lane.hpp): 0 = not eligible, else the register width NM
+    int lane_nm = 0, lane_blocks = 0;
+    size_t lane_shmem = 0;
+    double* lws = nullptr;     // saved Jacobians, slot-major [NM*NM][slots]
+    size_t lws_bytes = 0;
+    int* queue = nullptr;      // work counter
 };
 
 static thread_local std::string g_err;
@@ -1040,6 +1049,12 @@ int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs) {
     if (nrg) *nrg = m->nrg;
     if (nrs) *nrs = m->nrs;
     return 0;
+}
+
+int br_mech_engine(const br_mech* m) {
+    if (!m) return fail(BR_ERR_INPUT, "null mechanism");
+    const char* eng = getenv("BRHIP_ENGINE");
+    return (eng && strcmp(eng, "wave") == 0) ? 0 : m->lane_nm;
 }
 
 int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
@@ -1272,6 +1287,22 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     m->waves_per_cu = best_w;
     m->shmem = wg_lds_bytes(M, best);
     m->shmem1 = wg_lds_bytes(M, 1);
+    // ---- one-reactor-per-lane engine for small gas-only mechanisms (brhip_lane.hpp)
+    if (ns == 0 && n <= 12) {
+        m->lane_nm = n <= 9 ? 9 : 12;
+        const void* lfn = m->lane_nm == 9 ? (const void*)k_lane<9> : (const void*)k_lane<12>;
+        m->lane_shmem = lane_lds_bytes(m->lane_nm, n, M.nset, nrg, M.nfo);
+        int nb = 0;
+        if (m->lane_shmem > 64 * 1024 ||
+            hipFuncSetAttribute(lfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lfn, 64, m->lane_shmem) != hipSuccess || nb <= 0) {
+            m->lane_nm = 0;   // does not fit: the wave engine integrates it
+        } else {
+            int ncu = 0;
+            HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+            m->lane_blocks = nb * ncu;
+        }
+    }
     HIPCHK(hipEventCreate(&m->ev0));
     HIPCHK(hipEventCreate(&m->ev1));
     *out = m;
@@ -1284,6 +1315,8 @@ int br_mech_destroy(br_mech* m) {
     for (void* p : m->allocs) hipFree(p);
     if (m->ws) hipFree(m->ws);
     if (m->jws) hipFree(m->jws);
+    if (m->lws) hipFree(m->lws);
+    if (m->queue) hipFree(m->queue);
     if (m->ev0) hipEventDestroy(m->ev0);
     if (m->ev1) hipEventDestroy(m->ev1);
     delete m;
@@ -1411,6 +1444,33 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.trace_cap = (opts && trace) ? opts->trace_cap : 0;
     o.ufac = (opts && opts->unstable_factor != 0.0) ? opts->unstable_factor : 10.0;
     hipStream_t s = (hipStream_t)stream;
+    const char* eng = getenv("BRHIP_ENGINE");   // "wave" forces the wave-per-reactor engine
+    if (m->lane_nm && !trace && !(eng && strcmp(eng, "wave") == 0)) {
+        const int NM = m->lane_nm;
+        const int blocks = std::max(1, std::min((N + 63) / 64, m->lane_blocks));
+        const size_t need = (size_t)lane_lay(NM, m->n, m->dm.nset, m->nrg, m->dm.nfo).g_rows * blocks * 64 * sizeof(double);
+        if (need >= 0x7fffffffull) return fail(BR_ERR_UNSUPPORTED, "lane workspace exceeds the 2 GB buffer range");
+        if (m->lws_bytes < need) {
+            if (m->lws) hipFree(m->lws);
+            m->lws = nullptr; m->lws_bytes = 0;
+            HIPCHK(hipMalloc((void**)&m->lws, need));
+            m->lws_bytes = need;
+        }
+        if (!m->queue) HIPCHK(hipMalloc((void**)&m->queue, sizeof(int)));
+        HIPCHK(hipMemsetAsync(m->queue, 0, sizeof(int), s));
+        HIPCHK(hipEventRecord(m->ev0, s));
+        if (NM == 9) {
+            HIPCHK(hipFuncSetAttribute((const void*)k_lane<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem));
+            hipLaunchKernelGGL(k_lane<9>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue);
+        } else {
+            HIPCHK(hipFuncSetAttribute((const void*)k_lane<12>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem));
+            hipLaunchKernelGGL(k_lane<12>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(m->ev1, s));
+        m->ev_recorded = true;
+        return 0;
+    }
     HIPCHK(hipEventRecord(m->ev0, s));
     const int rpb = m->rpb;
     const dim3 grid((N + rpb - 1) / rpb), block(64 * rpb);

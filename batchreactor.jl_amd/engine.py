@@ -53,6 +53,17 @@ class Engine:
         self.n, self.ng, self.ns = mech.n, mech.ng, mech.ns
         self.nmax = 16 if self.n <= 16 else 32 if self.n <= 32 else 56 if self.n <= 56 else 64 if self.n <= 64 else 72   # kernel tile
 
+    @property
+    def kernel_name(self) -> str:
+        """the integrator kernel br_integrate_dev launches for this mechanism"""
+        nm = _lib.lib().br_mech_engine(self.h)
+        return f"k_lane<{nm}>" if nm > 0 else f"k_integrate<{self.nmax}>"
+
+    @property
+    def engine(self) -> str:
+        """'lane' (one reactor per lane, small gas mechanisms) or 'wave' (one reactor per wavefront)"""
+        return "lane" if _lib.lib().br_mech_engine(self.h) > 0 else "wave"
+
     def close(self):
         if getattr(self, "h", None):
             _lib.lib().br_mech_destroy(self.h)

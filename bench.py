@@ -146,7 +146,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "B per launch (PMC, profiles/traffic_gri.json)",
-                         "kernel": f"k_integrate<{eng.nmax}>", "kernel_ms": kernel_ms,
+                         "kernel": eng.kernel_name, "kernel_ms": kernel_ms,
                          "algorithmic_flop_per_launch": flops},
             "cpu_baseline": cpu,
             "solver": {"failed": nbad, "status_counts": {str(int(k)): int(np.sum(stats["status"] == k))

@@ -105,6 +105,11 @@ int         br_device_count(void);
 int br_mech_create(const br_mech_desc* desc, int device, br_mech** out);
 int br_mech_destroy(br_mech* m);
 int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs);
+/* integrator engine br_integrate* uses for this mechanism: 0 = one reactor per wavefront
+ * (k_integrate, analytic Jacobian), NM > 0 = one reactor per lane with NM-wide register tiles
+ * (k_lane, gas-only mechanisms with n <= 12, CVODE's DQ Jacobian as in the reference). Traced
+ * integrations always use the wavefront engine; env BRHIP_ENGINE=wave forces it. */
+int br_mech_engine(const br_mech* m);
 
 /* host-buffer entry points (copy in/out); arrays are reactor-major */
 int br_rates(br_mech* m, int N, const double* T, const double* p, const double* x /*[N][ng]*/,

@@ -348,3 +348,51 @@ def test_file_driven_gas_surf_profiles(pkg, gpu, tmp_path):
         assert np.max(np.abs(c[big] / rc[big] - 1)) < 1e-4, i
     dat = open(d / "gas_profile.dat").read().splitlines()
     assert len(dat) == len(gas) and dat[0].split() == hdr
+
+
+def test_lane_engine_h2o2(pkg, orc, gpu, monkeypatch):
+    """One-reactor-per-lane engine (k_lane: small gas mechanisms, CVODE's DQ Jacobian as the
+    reference's CVODE_BDF) against the oracle run with the same DQ Jacobian. N = 200 > 64 lanes
+    per wave, so lanes take new reactors from the work counter mid-run. Tight tolerances: end
+    states agree to 1e-6 relative; default tolerances: same status and, summed over the
+    ensemble, the same step / RHS / Jacobian counts to 10 % (rounding changes step sequences)."""
+    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    assert eng.engine == "lane"
+    N = 200
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", N, 6)
+    tf = np.where(np.arange(N) % 3 == 0, 1e-3, 1e-2)            # ragged end times
+    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16)
+    assert np.all(st["status"] == 0)
+    for i in range(N):
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf[i], analytic_jac=False, rtol=1e-10, atol=1e-16)
+        assert so["status"] == 0
+        e = close_states(U[i], uo, rtol=1e-6, floor=1e-14)
+        assert e <= 1.0, (i, e)
+    U, st = eng.integrate(T, Asv, U0, 1e-2)
+    Ud, std_, _ = om.integrate_batch(T, Asv, U0, 1e-2, analytic_jac=False, nthreads=8)
+    sd = np.array([s["status"] for s in std_])
+    assert np.array_equal(st["status"] == 0, sd == 0)
+    ok = (st["status"] == 0) & (sd == 0)
+    for key in ("nsteps", "nfe", "nje"):
+        g = float(st[key][ok].sum())
+        o = float(sum(std_[i][key] for i in np.nonzero(ok)[0]))
+        assert abs(g - o) <= 0.1 * o, (key, g, o)
+    assert np.max([close_states(U[i], Ud[i], rtol=1e-3) for i in np.nonzero(ok)[0]]) <= 1.0
+
+
+def test_lane_and_wave_engines_agree(pkg, gpu, monkeypatch):
+    """The two integrator engines (per-lane DQ Jacobian, per-wavefront analytic Jacobian) give the
+    same H2/O2 end states at tight tolerances."""
+    pm = pkg.Mechanism.from_files(LIB, gas_mech="h2o2.dat")
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", 96, 8)
+    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    eng = pkg.Engine(pm)
+    assert eng.engine == "lane"
+    Ul, sl = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    monkeypatch.setenv("BRHIP_ENGINE", "wave")
+    assert eng.engine == "wave"
+    Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    assert np.all(sl["status"] == 0) and np.all(sw["status"] == 0)
+    assert max(close_states(Ul[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(96)) <= 1.0
