@@ -41,6 +41,10 @@ enum { NO_FAILURES = 0, FAIL_BAD_J = 1, FAIL_OTHER = 2 };
 struct KOpts {
     double rtol, atol, hmax_inv, ufac;
     int max_steps, trace_cap;
+    int defer_steps;          // k_lane: hand a reactor still running after this many steps to the
+                              // wavefront engine (restart from u0); >= max_steps disables
+    const int* rid_list;      // k_integrate: integrate reactors rid_list[0 .. min(*rid_count, N)) only
+    const int* rid_count;
 };
 
 // ------------------------------------------------------------------------------------
@@ -763,8 +767,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     constexpr int VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
-    const int rid = W.rid;
-    if (rid >= N) return;
+    int rid = W.rid;
+    const int widx = rid;                 // workspace slot
+    if (o.rid_list) {                     // deferred reactors of a k_lane pass
+        if (rid >= min(*o.rid_count, N)) return;
+        rid = uni(o.rid_list[rid]);
+    } else if (rid >= N) {
+        return;
+    }
     const int lane = W.lane;
     const Tab& tb = W.tb;
     const size_t roff = (size_t)(W.rbase - smem_raw);
@@ -775,7 +785,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     const double T = Tv[rid];
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
-    double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
+    double* Jsave = Jws + (size_t)widx * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
     double* LUsave = Jsave + NMAX * VW;
     double* jscr = LUsave + lu_ws_doubles(NMAX);
     C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
@@ -1331,6 +1341,7 @@ static int ensure_ws(br_mech* m, size_t bytes) {
     m->ws_bytes = bytes;
     return 0;
 }
+constexpr int DEFER_CAP = 4096;   // reactors one k_lane pass may hand to the wavefront engine
 static int ensure_jws(br_mech* m, int N) {
     const size_t bytes = (size_t)N * ws_doubles(std::max(m->nmax, 64), m->nrg) * sizeof(double);
     if (m->jws_bytes >= bytes) return 0;
@@ -1434,8 +1445,6 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     if (!m || N < 0 || !dT || !du || !dtf) return fail(BR_ERR_INPUT, "bad argument");
     if (N == 0) return 0;
     HIPCHK(hipSetDevice(m->device));
-    int rc = ensure_jws(m, N);
-    if (rc) return rc;
     KOpts o;
     o.rtol = (opts && opts->rtol > 0) ? opts->rtol : 1e-6;
     o.atol = (opts && opts->atol > 0) ? opts->atol : 1e-10;
@@ -1443,9 +1452,15 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.hmax_inv = (opts && opts->hmax > 0) ? 1.0 / opts->hmax : 0.0;
     o.trace_cap = (opts && trace) ? opts->trace_cap : 0;
     o.ufac = (opts && opts->unstable_factor != 0.0) ? opts->unstable_factor : 10.0;
+    o.defer_steps = o.max_steps;
+    o.rid_list = nullptr;
+    o.rid_count = nullptr;
     hipStream_t s = (hipStream_t)stream;
     const char* eng = getenv("BRHIP_ENGINE");   // "wave" forces the wave-per-reactor engine
     if (m->lane_nm && !trace && !(eng && strcmp(eng, "wave") == 0)) {
+        // one reactor per lane; reactors still running after defer_steps steps (a few per 1e4 on
+        // H2/O2, some of them up to max_steps) are handed to a follow-up wavefront pass, whose
+        // per-step latency for a lone reactor is far lower than a wave's with one live lane
         const int NM = m->lane_nm;
         const int blocks = std::max(1, std::min((N + 63) / 64, m->lane_blocks));
         const size_t need = (size_t)lane_lay(NM, m->n, m->dm.nset, m->nrg, m->dm.nfo).g_rows * blocks * 64 * sizeof(double);
@@ -1456,21 +1471,40 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
             HIPCHK(hipMalloc((void**)&m->lws, need));
             m->lws_bytes = need;
         }
-        if (!m->queue) HIPCHK(hipMalloc((void**)&m->queue, sizeof(int)));
-        HIPCHK(hipMemsetAsync(m->queue, 0, sizeof(int), s));
+        const char* ds = getenv("BRHIP_DEFER_STEPS");
+        o.defer_steps = ds ? atoi(ds) : 5000;
+        if (o.defer_steps <= 0 || o.defer_steps >= o.max_steps) o.defer_steps = o.max_steps;
+        const int cap = std::min(N, DEFER_CAP);
+        int rc = ensure_jws(m, cap);
+        if (rc) return rc;
+        if (!m->queue) HIPCHK(hipMalloc((void**)&m->queue, (2 + DEFER_CAP) * sizeof(int)));
+        HIPCHK(hipMemsetAsync(m->queue, 0, 2 * sizeof(int), s));
         HIPCHK(hipEventRecord(m->ev0, s));
         if (NM == 9) {
             HIPCHK(hipFuncSetAttribute((const void*)k_lane<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem));
-            hipLaunchKernelGGL(k_lane<9>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue);
+            hipLaunchKernelGGL(k_lane<9>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue, cap);
         } else {
             HIPCHK(hipFuncSetAttribute((const void*)k_lane<12>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem));
-            hipLaunchKernelGGL(k_lane<12>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue);
+            hipLaunchKernelGGL(k_lane<12>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue, cap);
         }
         HIPCHK(hipGetLastError());
+        if (o.defer_steps < o.max_steps) {   // the deferred reactors, from u0, on the wavefront engine
+            KOpts o2 = o;
+            o2.defer_steps = o.max_steps;
+            o2.rid_list = m->queue + 2;
+            o2.rid_count = m->queue + 1;
+            const int rpb = m->rpb;
+            HIPCHK(hipFuncSetAttribute((const void*)k_integrate<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem));
+            hipLaunchKernelGGL(k_integrate<16>, dim3((cap + rpb - 1) / rpb), dim3(64 * rpb), m->shmem, s, m->dm, cap, rpb, dT,
+                               dAsv, du, dtf, o2, (double*)dstats, m->jws, (double*)nullptr);
+            HIPCHK(hipGetLastError());
+        }
         HIPCHK(hipEventRecord(m->ev1, s));
         m->ev_recorded = true;
         return 0;
     }
+    int rc = ensure_jws(m, N);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(m->ev0, s));
     const int rpb = m->rpb;
     const dim3 grid((N + rpb - 1) / rpb), block(64 * rpb);

@@ -115,6 +115,7 @@ struct ZH {
 
 enum { PH_JAC = 4 };
 enum { A_NONE = 7 };
+constexpr int ST_DEFER = 1;   // lane status: hand the reactor to the wavefront pass
 enum { PEND_NONE = 0, PEND_STEP = 1, PEND_ATTEMPT = 2, PEND_ADJ = 3, PEND_EF1 = 4 };
 
 // per-lane CVODE scalars (cv_mem)
@@ -687,6 +688,7 @@ __device__ __forceinline__ int l_post_solve(LCV& c, ZH<NM>& z, double (&acor)[NM
         c.eta = c.hprime / h;
     }
     if (c.nstloc >= o.max_steps) { c.status = BR_ERR_MAXSTEPS; return A_DONE; }
+    if (c.nstloc == o.defer_steps) { c.status = ST_DEFER; return A_DONE; }   // kernel decides
     c.pend = PEND_STEP;
     return A_RHS;
 }
@@ -927,7 +929,8 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
 template <int NM>
 __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __restrict__ Tv, double* __restrict__ U,
                                              const double* __restrict__ tfv, KOpts o, double* __restrict__ stats,
-                                             double* __restrict__ Jg, int* __restrict__ queue) {
+                                             double* __restrict__ Jg, int* __restrict__ queue, int defer_cap) {
+    // queue[0]: next reactor; queue[1]: deferred count; queue[2 ..]: deferred reactor ids
     const int lane = threadIdx.x;
     const int n = MF(n);
     const LaneLay LL = lane_lay(NM, n, MF(nset), MF(nrg), MF(nfo));
@@ -1038,6 +1041,18 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
         if (act == A_SOLVE || act == A_SETUP) act = l_post_solve<NM>(c, z, acor, ewt, y, b, lu_fail, o, n);
         if (act == A_RHS && c.pend != PEND_NONE) l_run_pending<NM>(c, z, acor, ewt, y, o, n);
         LACC(k_ctl, t5);
+        if (act == A_DONE && c.status == ST_DEFER) {
+            const int di = atomicAdd(queue + 1, 1);
+            if (di < defer_cap) {
+                queue[2 + di] = rid;                         // U[rid] still holds u0
+                has = false;
+            } else {                                         // no room: keep integrating here
+                c.status = 0;
+                c.pend = PEND_STEP;
+                l_run_pending<NM>(c, z, acor, ewt, y, o, n);
+            }
+            act = A_RHS;
+        }
         if (act == A_DONE) {
             const int status = c.status;
 #pragma unroll

@@ -396,3 +396,26 @@ def test_lane_and_wave_engines_agree(pkg, gpu, monkeypatch):
     Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
     assert np.all(sl["status"] == 0) and np.all(sw["status"] == 0)
     assert max(close_states(Ul[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(96)) <= 1.0
+
+
+def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
+    """Reactors still running after BRHIP_DEFER_STEPS steps in the lane engine are handed to the
+    wavefront engine, which restarts them from u0 (the lane pass leaves u untouched for them).
+    With the threshold at 30 steps most of the 300 reactors take that path; every end state must
+    still match the oracle at tight tolerances, and the step counts must be the full ones."""
+    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    monkeypatch.setenv("BRHIP_DEFER_STEPS", "30")
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    assert eng.engine == "lane"
+    N = 300
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", N, 11)
+    tf = np.where(np.arange(N) % 2 == 0, 1e-6, 1e-2)          # short runs stay on the lanes
+    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16)
+    assert np.all(st["status"] == 0)
+    assert np.sum(st["nsteps"] > 30) > N // 3
+    for i in range(N):
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf[i], analytic_jac=False, rtol=1e-10, atol=1e-16)
+        assert close_states(U[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, i
+        if st["nsteps"][i] > 30:
+            assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.2 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
