@@ -87,19 +87,19 @@ struct ZH {
     double* Lz;     // this lane's LDS row base for z2: element (j, i) at Lz[((j - 2) * NM + i) * 64]
     int n;
     __device__ __forceinline__ double get(int j, int i) const {
-        return j == 0 ? z0[i] : (j == 1 ? z1[i] : (i < n ? Lz[((j - 2) * NM + i) * 64] : 0.0));
+        return j == 0 ? z0[i] : (j == 1 ? z1[i] : Lz[((j - 2) * NM + i) * 64]);   // pad rows hold 0
     }
     __device__ __forceinline__ void set(int j, int i, double v) {
         if (j == 0) z0[i] = v;
         else if (j == 1) z1[i] = v;
-        else if (i < n) Lz[((j - 2) * NM + i) * 64] = v;
+        else Lz[((j - 2) * NM + i) * 64] = v;
     }
     // row j (per-lane j) into out
     __device__ __forceinline__ void row(int j, double (&out)[NM]) const {
         const int jj = j < 2 ? 2 : j;
 #pragma unroll
         for (int i = 0; i < NM; ++i) {
-            const double lv = (i < n) ? Lz[((jj - 2) * NM + i) * 64] : 0.0;
+            const double lv = Lz[((jj - 2) * NM + i) * 64];
             out[i] = j == 0 ? z0[i] : (j == 1 ? z1[i] : lv);
         }
     }
@@ -165,39 +165,47 @@ __device__ __forceinline__ double lwrms(const double (&v)[NM], const double (&w)
 //      increase_bdf / decrease_bdf), unrolled over QMAX with per-lane order predicates
 template <int NM>
 __device__ __forceinline__ void l_rescale(LCV& c, ZH<NM>& z) {
+    double fj[QMAX + 1];                             // eta^j for rows j <= q, 1 above (x * 1 = x)
     double factor = c.eta;
 #pragma unroll
     for (int j = 1; j <= QMAX; ++j) {
-        if (j <= c.q) {
-#pragma unroll
-            for (int i = 0; i < NM; ++i) z.set(j, i, z.get(j, i) * factor);
-            factor *= c.eta;
-        }
+        fj[j] = (j <= c.q) ? factor : 1.0;
+        factor *= c.eta;
     }
+#pragma unroll
+    for (int j = 1; j <= QMAX; ++j)
+#pragma unroll
+        for (int i = 0; i < NM; ++i) z.set(j, i, z.get(j, i) * fj[j]);
     c.h = c.hscale * c.eta;
     c.hscale = c.h;
 }
+// Nordsieck prediction z <- P z (P the Pascal matrix of order q) and its inverse, as one
+// matrix-vector product per component with per-lane masked binomial coefficients: z_j += sum_{i>j,
+// i<=q} (+-)C(i,j) z_i (CVODE's repeated row additions, same values up to rounding)
 template <int NM, bool SUB>
 __device__ __forceinline__ void l_pascal(const LCV& c, ZH<NM>& z) {
+    constexpr double BIN[QMAX + 1][QMAX + 1] = {{1, 1, 1, 1, 1, 1}, {0, 1, 2, 3, 4, 5}, {0, 0, 1, 3, 6, 10},
+                                                {0, 0, 0, 1, 4, 10}, {0, 0, 0, 0, 1, 5}, {0, 0, 0, 0, 0, 1}};
+    double cf[QMAX][QMAX + 1];                       // cf[j][i], i > j
 #pragma unroll
-    for (int i = 0; i < NM; ++i) {               // component by component: 6 live values
+    for (int i = 1; i <= QMAX; ++i) {
+        const double mi = (i <= c.q) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < i; ++j) cf[j][i] = ((SUB && ((i - j) & 1)) ? -BIN[j][i] : BIN[j][i]) * mi;
+    }
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
         double r[QMAX + 1];
-        r[0] = z.z0[i];
-        r[1] = z.z1[i];
 #pragma unroll
-        for (int j = 2; j <= QMAX; ++j) r[j] = z.get(j, i);
+        for (int j = 0; j <= QMAX; ++j) r[j] = z.get(j, k);
 #pragma unroll
-        for (int k = 1; k <= QMAX; ++k)
+        for (int j = 0; j < QMAX; ++j) {
+            double acc = r[j];
 #pragma unroll
-            for (int j = QMAX; j >= k; --j)
-            {
-                const double v = (j <= c.q) ? r[j] : 0.0;   // x +- 0 = x: no branch
-                r[j - 1] = SUB ? r[j - 1] - v : r[j - 1] + v;
-            }
-        z.z0[i] = r[0];
-        z.z1[i] = r[1];
-#pragma unroll
-        for (int j = 2; j < QMAX; ++j) if (j < c.q) z.set(j, i, r[j]);
+            for (int i = j + 1; i <= QMAX; ++i) acc = fma(cf[j][i], r[i], acc);
+            if (j < 2) z.set(j, k, acc);
+            else if (j < c.q) z.set(j, k, acc);
+        }
     }
 }
 template <int NM>
@@ -211,15 +219,20 @@ __device__ __forceinline__ void l_restore(LCV& c, ZH<NM>& z) {
     c.tn = c.saved_t;
     l_pascal<NM, true>(c, z);
 }
+// cvAdjustOrder (oracle/oracle.c increase_bdf / decrease_bdf): the coefficient recurrences per
+// lane, then ONE pass over the components for both directions:
+//   increase: z[q+1] = A1 z5, z[j] += l[j] z[q+1] (2 <= j <= q);  decrease: z[j] -= l[j] z[q] (2 <= j < q)
 template <int NM>
 __device__ __forceinline__ void l_adjust_order(LCV& c, ZH<NM>& z, int dq) {
     const int q = c.q;
-    if ((q == 2) && (dq != 1)) return;
+    const bool inc = dq == 1;
+    const bool act = inc || q > 2;                   // cvAdjustOrder: nothing for q == 2 going down
     double* l = c.l;
 #pragma unroll
     for (int i = 0; i <= QMAX + 1; ++i) l[i] = 0.0;
     l[2] = 1.0;
-    if (dq == 1) {                                    // increase_bdf
+    double A1 = 0.0;
+    if (inc) {                                        // increase_bdf coefficients
         double alpha1 = 1.0, prod = 1.0, xiold = 1.0, alpha0 = -1.0, hsum = c.hscale;
 #pragma unroll
         for (int j = 1; j < QMAX - 1; ++j) {
@@ -234,17 +247,8 @@ __device__ __forceinline__ void l_adjust_order(LCV& c, ZH<NM>& z, int dq) {
                 xiold = xi;
             }
         }
-        const double A1 = (-alpha0 - alpha1) / prod;
-        const int L = q + 1;
-#pragma unroll
-        for (int i = 0; i < NM; ++i) {
-            const double zl = A1 * z.get(QMAX, i);
-#pragma unroll
-            for (int j = 2; j <= QMAX; ++j) if (j == L) z.set(j, i, zl);
-#pragma unroll
-            for (int j = 2; j <= QMAX; ++j) if (j <= q) z.set(j, i, z.get(j, i) + l[j] * zl);
-        }
-    } else {                                          // decrease_bdf
+        A1 = (-alpha0 - alpha1) / prod;
+    } else {                                          // decrease_bdf coefficients
         double hsum = 0.0;
 #pragma unroll
         for (int j = 1; j <= QMAX - 2; ++j) {
@@ -255,14 +259,26 @@ __device__ __forceinline__ void l_adjust_order(LCV& c, ZH<NM>& z, int dq) {
                 for (int i = j + 2; i >= 2; --i) l[i] = l[i] * xi + l[i - 1];
             }
         }
-        double zq[NM];
-        z.row(q, zq);
+    }
+    double cf[QMAX + 1];
 #pragma unroll
-        for (int j = 2; j < QMAX; ++j)
-            if (j < q) {
+    for (int j = 2; j <= QMAX; ++j)
+        cf[j] = !act ? 0.0 : (inc ? ((j <= q) ? l[j] : 0.0) : ((j < q) ? -l[j] : 0.0));
+    const int L = inc ? q + 1 : -1;
 #pragma unroll
-                for (int i = 0; i < NM; ++i) z.set(j, i, z.get(j, i) - l[j] * zq[i]);
-            }
+    for (int i = 0; i < NM; ++i) {
+        double r[QMAX + 1];
+#pragma unroll
+        for (int j = 2; j <= QMAX; ++j) r[j] = z.get(j, i);
+        double zq = r[2];
+#pragma unroll
+        for (int j = 3; j <= QMAX; ++j) zq = (q == j) ? r[j] : zq;
+        const double src = inc ? A1 * r[QMAX] : zq;
+#pragma unroll
+        for (int j = 2; j <= QMAX; ++j) {
+            const double v = (j == L) ? src : fma(cf[j], src, r[j]);
+            if (act) z.set(j, i, v);
+        }
     }
 }
 
@@ -760,17 +776,26 @@ __device__ __forceinline__ void l_getrs(const GRows& G, const LaneLay& LL, unsig
             b[k] = bp;
         }
     }
+    // all factors in one burst of loads (one exposed latency), then the sweeps
+    double lu[NM][NM], rp[NM];
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+        rp[k] = G.ld(LL.g_rpv + k);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) lu[k][i] = (i != k) ? G.ld(LL.g_lu + k * NM + i) : 0.0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < NM - 1; ++k)
 #pragma unroll
-        for (int i = k + 1; i < NM; ++i) b[i] -= G.ld(LL.g_lu + k * NM + i) * b[k];
+        for (int i = k + 1; i < NM; ++i) b[i] -= lu[k][i] * b[k];
 #pragma unroll
     for (int k = NM - 1; k > 0; --k) {
-        b[k] *= G.ld(LL.g_rpv + k);
+        b[k] *= rp[k];
 #pragma unroll
-        for (int i = 0; i < k; ++i) b[i] -= G.ld(LL.g_lu + k * NM + i) * b[k];
+        for (int i = 0; i < k; ++i) b[i] -= lu[k][i] * b[k];
     }
-    b[0] *= G.ld(LL.g_rpv);
+    b[0] *= rp[0];
 }
 
 // ---- rates: T-only constants per lane (at reactor start) and the gas-phase RHS
@@ -1015,12 +1040,14 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
                 const double mg = -c.gamma;
                 double a[NM][NM], rpv[NM];
 #pragma unroll
-                for (int j = 0; j < NM; ++j) {
+                for (int j = 0; j < NM; ++j)
 #pragma unroll
-                    for (int i = 0; i < NM; ++i)
-                        a[i][j] = (i < n && j < n) ? G.ld(j * NM + i) * mg + (i == j ? 1.0 : 0.0)
-                                                   : (i == j ? 1.0 : 0.0);
-                }
+                    for (int i = 0; i < NM; ++i) a[i][j] = (i < n && j < n) ? G.ld(j * NM + i) : 0.0;
+                __builtin_amdgcn_sched_barrier(0);   // one burst of loads, then the factorisation
+#pragma unroll
+                for (int j = 0; j < NM; ++j)
+#pragma unroll
+                    for (int i = 0; i < NM; ++i) a[i][j] = a[i][j] * mg + (i == j ? 1.0 : 0.0);
                 lu_fail = l_getrf<NM>(a, pv, rpv);
 #pragma unroll
                 for (int j = 0; j < NM; ++j) {
