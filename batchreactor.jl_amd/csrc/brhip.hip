@@ -45,6 +45,8 @@ struct KOpts {
                               // wavefront engine (restart from u0); >= max_steps disables
     const int* rid_list;      // k_integrate: integrate reactors rid_list[0 .. min(*rid_count, N)) only
     const int* rid_count;
+    int* work;                // k_integrate: persistent waves take reactor indices from this
+                              // counter (nullptr: one reactor per wave, index = wave slot)
 };
 
 // ------------------------------------------------------------------------------------
@@ -767,14 +769,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
     constexpr int VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
-    int rid = W.rid;
-    const int widx = rid;                 // workspace slot
-    if (o.rid_list) {                     // deferred reactors of a k_lane pass
-        if (rid >= min(*o.rid_count, N)) return;
-        rid = uni(o.rid_list[rid]);
-    } else if (rid >= N) {
-        return;
-    }
+    // Reactor indices: with o.work every wave of the (resident-sized) grid keeps taking the next
+    // index from the counter until the list is drained, so a wave whose reactor finishes early
+    // starts another instead of idling until the slowest reactor of its workgroup is done; the
+    // wave's workspace slot and LDS block are reused. Index -> reactor through rid_list when set
+    // (the deferred reactors of a k_lane pass).
+    const int widx = W.rid;               // workspace slot of this wave
+    const int nidx = o.rid_list ? min(*o.rid_count, N) : N;
+    auto next_index = [&]() -> int {
+        int v = 0;
+        if (W.lane == 0) v = atomicAdd(o.work, 1);
+        return __builtin_amdgcn_readlane(v, 0);
+    };
+    for (int idx = o.work ? next_index() : widx; idx < nidx; idx = o.work ? next_index() : nidx) {
+    int rid = o.rid_list ? uni(o.rid_list[idx]) : idx;
+    wave_sync();
     const int lane = W.lane;
     const Tab& tb = W.tb;
     const size_t roff = (size_t)(W.rbase - smem_raw);
@@ -903,6 +912,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))
 #endif
         st[13] = ud(C->tn);
     }
+    }   // next reactor
 }
 
 // ------------------------------------------------------------------------------------
@@ -1020,6 +1030,8 @@ struct br_mech {
     double* lws = nullptr;     // saved Jacobians, slot-major [NM*NM][slots]
     size_t lws_bytes = 0;
     int* queue = nullptr;      // work counter
+    int* wq = nullptr;         // k_integrate work counter
+    int ncu = 0;
 };
 
 static thread_local std::string g_err;
@@ -1295,6 +1307,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     if (best_w == 0) { br_mech_destroy(m); return fail(BR_ERR_UNSUPPORTED, "mechanism too large for LDS"); }
     m->rpb = best;
     m->waves_per_cu = best_w;
+    HIPCHK(hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, device));
     m->shmem = wg_lds_bytes(M, best);
     m->shmem1 = wg_lds_bytes(M, 1);
     // ---- one-reactor-per-lane engine for small gas-only mechanisms (brhip_lane.hpp)
@@ -1327,6 +1340,7 @@ int br_mech_destroy(br_mech* m) {
     if (m->jws) hipFree(m->jws);
     if (m->lws) hipFree(m->lws);
     if (m->queue) hipFree(m->queue);
+    if (m->wq) hipFree(m->wq);
     if (m->ev0) hipEventDestroy(m->ev0);
     if (m->ev1) hipEventDestroy(m->ev1);
     delete m;
@@ -1455,6 +1469,7 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.defer_steps = o.max_steps;
     o.rid_list = nullptr;
     o.rid_count = nullptr;
+    o.work = nullptr;
     hipStream_t s = (hipStream_t)stream;
     const char* eng = getenv("BRHIP_ENGINE");   // "wave" forces the wave-per-reactor engine
     if (m->lane_nm && !trace && !(eng && strcmp(eng, "wave") == 0)) {
@@ -1503,11 +1518,22 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
         m->ev_recorded = true;
         return 0;
     }
-    int rc = ensure_jws(m, N);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(m->ev0, s));
     const int rpb = m->rpb;
-    const dim3 grid((N + rpb - 1) / rpb), block(64 * rpb);
+    // persistent grid: as many workgroups as are resident at once, reactors from a work counter
+    // (BRHIP_STATIC=1: one reactor per wave over ceil(N / rpb) workgroups)
+    const char* st_env = getenv("BRHIP_STATIC");
+    const bool dyn = !(st_env && atoi(st_env) == 1) && m->ncu > 0 && m->waves_per_cu >= rpb;
+    const int nwg_all = (N + rpb - 1) / rpb;
+    const int nwg = dyn ? std::min(nwg_all, m->ncu * (m->waves_per_cu / rpb)) : nwg_all;
+    int rc = ensure_jws(m, nwg * rpb);
+    if (rc) return rc;
+    if (dyn) {
+        if (!m->wq) HIPCHK(hipMalloc((void**)&m->wq, sizeof(int)));
+        HIPCHK(hipMemsetAsync(m->wq, 0, sizeof(int), s));
+        o.work = m->wq;
+    }
+    HIPCHK(hipEventRecord(m->ev0, s));
+    const dim3 grid(nwg), block(64 * rpb);
     if (m->nmax == 16) {
         HIPCHK(hipFuncSetAttribute((const void*)k_integrate<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem));
         hipLaunchKernelGGL(k_integrate<16>, grid, block, m->shmem, s, m->dm, N, rpb, dT, dAsv, du, dtf, o, (double*)dstats, m->jws, trace);
