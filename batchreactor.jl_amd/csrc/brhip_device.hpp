@@ -824,15 +824,23 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 // Two register buffers alternate: each chunk's loads are issued a full chunk ahead of use.
 template <bool FWD>
 __device__ __forceinline__ void tri_chunk(const double (&v)[8], int c, int lo, int n, double& r) {
+    // the lane masks zero the factor entries up front (off the r dependency chain): a lane that
+    // must not update adds -0 * x, which leaves r unchanged, so the chain per column is just
+    // fma -> readlane -> fma (x = r[k] is finite whenever the solve is)
+    double vm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = c + i;
+        // forward: lo = lane (lanes >= n: -1); backward: lo = lane, limit min(k, n) with k >= n -> none
+        const bool upd = FWD ? (lo > k) : (lo < ((k < n) ? k : 0));
+        vm[i] = upd ? v[i] : 0.0;
+    }
 #pragma unroll
     for (int ii = 0; ii < 8; ++ii) {
         const int i = FWD ? ii : 7 - ii;
         const int k = c + i;
         const double x = bcast(r, k < n ? k : 0);
-        // forward: lo = lane (lanes >= n: -1); backward: lo = lane, limit min(k, n) with k >= n -> none
-        const bool upd = FWD ? (lo > k) : (lo < ((k < n) ? k : 0));
-        const double t = fma(-v[i], x, r);
-        r = upd ? t : r;
+        r = fma(-vm[i], x, r);
     }
 }
 template <bool FWD>
@@ -1081,18 +1089,24 @@ __device__ __forceinline__ void tri_sweep2(const BR_GLOBAL double* __restrict__ 
     for (int t = 0; t < NCH; ++t) {
         __builtin_amdgcn_sched_barrier(0);
         const int c = cidx(t);
+        // masks applied to the factor entries, off the r chain (see tri_chunk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = c + i;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int row = lane + 64 * s;
+                const bool upd = FWD ? (row > k && row < n) : (row < k && k < n);
+                v[t & 1][s][i] = upd ? v[t & 1][s][i] : 0.0;
+            }
+        }
 #pragma unroll
         for (int ii = 0; ii < 8; ++ii) {
             const int i = FWD ? ii : 7 - ii;
             const int k = c + i;
             const double x = bcast(r[k >> 6], k & 63);
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int row = lane + 64 * s;
-                const bool upd = FWD ? (row > k && row < n) : (row < k && k < n);
-                const double tt = fma(-v[t & 1][s][i], x, r[s]);
-                r[s] = upd ? tt : r[s];
-            }
+            for (int s = 0; s < 2; ++s) r[s] = fma(-v[t & 1][s][i], x, r[s]);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (t + 2 < NCH) load(v[t & 1], cidx(t + 2));
