@@ -112,8 +112,8 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
 }
 
 // uniform loads from the LDS controller
-__device__ __forceinline__ double ud(const volatile LDbl& x) { return uni((double)x); }
-__device__ __forceinline__ int ui(const volatile __attribute__((address_space(3))) int& x) { return uni((int)x); }
+__device__ __forceinline__ double ud(const LDbl& x) { return uni((double)x); }
+__device__ __forceinline__ int ui(const __attribute__((address_space(3))) int& x) { return uni((int)x); }
 
 #ifndef BR_CTL_INLINE
 #define BR_CTL_INLINE __forceinline__
