@@ -419,3 +419,24 @@ def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
         assert close_states(U[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, i
         if st["nsteps"][i] > 30:
             assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.2 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
+
+
+@pytest.mark.parametrize("case,N", [("gri", 3000), ("surf", 5000)])
+def test_persistent_grid_matches_static(pkg, gpu, monkeypatch, case, N):
+    """k_integrate's persistent grid (waves take reactors from a work counter, reusing their LDS
+    block and workspace slot) gives bit-identical end states and counters to the one-reactor-per-
+    wave grid (BRHIP_STATIC=1): each reactor's arithmetic does not depend on which wave or slot
+    ran it. N exceeds the resident wave count, so slots are reused many times."""
+    gas = {"gri": "grimech.dat", "surf": None}[case]
+    pm = pkg.Mechanism.from_files(LIB, gas_mech=gas, surface_mech="ch4ni.xml" if case == "surf" else None,
+                                  gasphase=None if gas else "CH4 H2O H2 CO CO2 O2 N2".split())
+    from batchreactor_amd import ensemble
+    T, Asv, U0 = ensemble.make_inputs(pm, case, 0, N)
+    eng = pkg.Engine(pm)
+    monkeypatch.delenv("BRHIP_STATIC", raising=False)
+    Ud, sd = eng.integrate(T, Asv, U0, 10.0)
+    monkeypatch.setenv("BRHIP_STATIC", "1")
+    Us, ss = eng.integrate(T, Asv, U0, 10.0)
+    assert np.array_equal(Ud, Us)
+    for k in ("nsteps", "nfe", "nje", "nsetups", "netf", "status"):
+        assert np.array_equal(sd[k], ss[k]), k
