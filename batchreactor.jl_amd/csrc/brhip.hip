@@ -760,8 +760,11 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (
 #ifndef BR_WPE
 #define BR_WPE 2
 #endif
+#ifndef BR_MAXRPB
+#define BR_MAXRPB 4   // reactors (waves) per workgroup, upper bound for the occupancy search
+#endif
 template <int NMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))) void k_integrate(
+__global__ __launch_bounds__(64 * BR_MAXRPB) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))) void k_integrate(
     DevMech M, int N, int rpb, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
     const double* __restrict__ tfv, KOpts o, double* __restrict__ stats, double* __restrict__ Jws,
     double* __restrict__ trace) {
@@ -1296,7 +1299,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
                     : m->nmax == 56 ? (const void*)k_integrate<56>
                     : m->nmax == 64 ? (const void*)k_integrate<64> : (const void*)k_integrate<72>;
     int best = 0, best_w = 0;
-    for (int rpb = 1; rpb <= 4; ++rpb) {
+    for (int rpb = 1; rpb <= BR_MAXRPB; ++rpb) {
         const size_t b = wg_lds_bytes(M, rpb);
         if (b > 160 * 1024) break;
         if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) != hipSuccess) break;
