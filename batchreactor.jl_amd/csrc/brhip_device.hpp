@@ -852,19 +852,24 @@ __device__ __forceinline__ void tri_load(double (&v)[8], const BR_GLOBAL double*
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = p[i * WAVE];
 }
+#ifndef BR_TRI_DEPTH
+#define BR_TRI_DEPTH 3   // register buffers of 8 columns in flight (loads DEPTH-1 chunks ahead)
+#endif
 template <bool FWD, int NCH>
 __device__ __forceinline__ double tri_sweep(const BR_GLOBAL double* __restrict__ col, int lane, int n, double r) {
-    double A[2][8];
+    constexpr int DB = BR_TRI_DEPTH;
+    double A[DB][8];
     auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
     const int lo = FWD ? ((lane < n) ? lane : -1) : lane;
-    tri_load<FWD>(A[0], col, cidx(0), lane, n);
-    if (NCH > 1) tri_load<FWD>(A[1], col, cidx(1), lane, n);
+#pragma unroll
+    for (int t = 0; t < DB - 1; ++t)
+        if (t < NCH) tri_load<FWD>(A[t], col, cidx(t), lane, n);
 #pragma unroll
     for (int t = 0; t < NCH; ++t) {          // fully unrolled: exact vmcnt waits for the prefetch
-        __builtin_amdgcn_sched_barrier(0);   // loads stay a full chunk ahead of their use
-        tri_chunk<FWD>(A[t & 1], cidx(t), lo, n, r);
+        __builtin_amdgcn_sched_barrier(0);   // loads stay DB-1 chunks ahead of their use
+        if (t + DB - 1 < NCH) tri_load<FWD>(A[(t + DB - 1) % DB], col, cidx(t + DB - 1), lane, n);
         __builtin_amdgcn_sched_barrier(0);
-        if (t + 2 < NCH) tri_load<FWD>(A[t & 1], col, cidx(t + 2), lane, n);
+        tri_chunk<FWD>(A[t % DB], cidx(t), lo, n, r);
     }
     return r;
 }
@@ -876,11 +881,29 @@ template <int NMAX>
 __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n, int lane, int perm, double b) {
     const BR_GLOBAL double* wsg = launder(ws);
     lane = launder_v(lane);
-    constexpr int NCH = NMAX / 8;
+    // the forward (unit lower) and backward (unit upper) sweeps run as ONE chunk sequence with
+    // one prefetch pipeline, so the backward sweep's first columns and D^-1 are already in
+    // flight while the forward sweep finishes (the factors come from L2 / Infinity Cache)
+    constexpr int NCH = NMAX / 8, NT = 2 * NCH, DB = BR_TRI_DEPTH;
+    double A[DB][8];
+    auto load = [&](int t) {
+        if (t < NCH) tri_load<true>(A[t % DB], wsg, t * 8, lane, n);
+        else tri_load<false>(A[t % DB], wsg, (NT - 1 - t) * 8, lane, n);
+    };
+    const double dinv = wsg[NMAX * WAVE + lane];   // D^-1
     double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
-    r = tri_sweep<true, NCH>(wsg, lane, n, r);     // forward, unit lower
-    r *= wsg[NMAX * WAVE + lane];                  // D^-1
-    r = tri_sweep<false, NCH>(wsg, lane, n, r);    // backward, unit upper
+    const int lo = (lane < n) ? lane : -1;
+#pragma unroll
+    for (int t = 0; t < DB - 1; ++t) load(t);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + DB - 1 < NT) load(t + DB - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t < NCH) tri_chunk<true>(A[t % DB], t * 8, lo, n, r);
+        else tri_chunk<false>(A[t % DB], (NT - 1 - t) * 8, lane, n, r);
+        if (t == NCH - 1) r *= dinv;
+    }
     return (lane < n) ? r : 0.0;
 }
 
