@@ -685,11 +685,14 @@ struct LUWs {
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
 // entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane =
 // original row), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
+#ifndef BR_LU_CH
+#define BR_LU_CH 8   // 4: 63.9k, 2: 62.8k, 8: 64.1k GRI reactors/s (scalar branch per chunk)
+#endif
 template <int W>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
                                             double& dinv, int& fail, const LUWs& F) {
-    constexpr int CH = 8;
-    static_assert(W % CH == 0, "W must be a multiple of 8");
+    constexpr int CH = BR_LU_CH;   // live-column granularity of the rank-1 update
+    static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
         const int p = pivot_lane(fabs(a[0]), pstep < 0);

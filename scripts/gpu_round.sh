@@ -19,7 +19,7 @@ STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *tests* ]] && run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 [[ $STEPS == *bench* ]] && run bench 900 python3 bench.py ${BENCH_ARGS:-}
-[[ $STEPS == *prof* ]] && run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${PROF_ARGS:---n 20000 --steps 2 --warmup 1}
+[[ $STEPS == *prof* ]] && run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${PROF_ARGS:---steps 3 --warmup 1}
 if [[ $STEPS == *pmc* ]]; then   # HBM traffic of k_integrate: separate counter passes (no tracing)
   PN=${PMC_N:-20000}
   run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- python3 bench.py --no-cpu --n $PN --steps 1 --warmup 0
