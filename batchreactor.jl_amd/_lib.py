@@ -33,7 +33,7 @@ class Opts(C.Structure):
 NSTAT = 16
 
 
-EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info", "br_mech_engine",
+EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info", "br_mech_engine", "br_mech_launch_info",
            "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_traced", "br_integrate_dev",
            "br_last_kernel_ms", "br_debug_lu_solve"]
 
@@ -56,6 +56,7 @@ def lib():
     L.br_mech_info.argtypes = [vp, ip, ip, ip, ip]
     L.br_mech_engine.argtypes = [vp]
     L.br_mech_engine.restype = C.c_int
+    L.br_mech_launch_info.argtypes = [vp, ip, ip, C.POINTER(C.c_longlong)]
     L.br_rates.argtypes = [vp, C.c_int, dp, dp, dp, dp, dp, dp]
     L.br_rhs.argtypes = [vp, C.c_int, dp, dp, dp, dp]
     L.br_jacobian.argtypes = [vp, C.c_int, dp, dp, dp, dp]

@@ -760,11 +760,13 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (
 #ifndef BR_WPE
 #define BR_WPE 2
 #endif
-#ifndef BR_MAXRPB
-#define BR_MAXRPB 4   // reactors (waves) per workgroup, upper bound for the occupancy search
-#endif
+// upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
+// needs ~26 KB of LDS per reactor, so only one workgroup of up to 5 reactors (tables staged once)
+// fits a CU's 160 KB: 5 waves/CU instead of 4 with 1-reactor workgroups (C5 10.7k -> 12.4k/s);
+// n <= 64 keeps 256-thread workgroups (2 x 4 or 4 x 2 reactors, 8 waves/CU, VGPR-limited)
+__host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 5 : 4; }
 template <int NMAX>
-__global__ __launch_bounds__(64 * BR_MAXRPB) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))) void k_integrate(
+__global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))) void k_integrate(
     DevMech M, int N, int rpb, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
     const double* __restrict__ tfv, KOpts o, double* __restrict__ stats, double* __restrict__ Jws,
     double* __restrict__ trace) {
@@ -1082,6 +1084,14 @@ int br_mech_engine(const br_mech* m) {
     return (eng && strcmp(eng, "wave") == 0) ? 0 : m->lane_nm;
 }
 
+int br_mech_launch_info(const br_mech* m, int* rpb, int* waves_per_cu, long long* lds_bytes) {
+    if (!m) return fail(BR_ERR_INPUT, "null mechanism");
+    if (rpb) *rpb = m->rpb;
+    if (waves_per_cu) *waves_per_cu = m->waves_per_cu;
+    if (lds_bytes) *lds_bytes = (long long)m->shmem;
+    return 0;
+}
+
 int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     if (!d || !out) return fail(BR_ERR_INPUT, "null argument");
     const int ng = d->ng, ns = d->ns, nrg = d->nrg, nrs = d->nrs, n = ng + ns;
@@ -1299,7 +1309,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
                     : m->nmax == 56 ? (const void*)k_integrate<56>
                     : m->nmax == 64 ? (const void*)k_integrate<64> : (const void*)k_integrate<72>;
     int best = 0, best_w = 0;
-    for (int rpb = 1; rpb <= BR_MAXRPB; ++rpb) {
+    for (int rpb = 1; rpb <= br_maxrpb(m->nmax); ++rpb) {
         const size_t b = wg_lds_bytes(M, rpb);
         if (b > 160 * 1024) break;
         if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) != hipSuccess) break;

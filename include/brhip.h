@@ -110,6 +110,10 @@ int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs);
  * (k_lane, gas-only mechanisms with n <= 12, CVODE's DQ Jacobian as in the reference). Traced
  * integrations always use the wavefront engine; env BRHIP_ENGINE=wave forces it. */
 int br_mech_engine(const br_mech* m);
+/* launch geometry of the wavefront engine for this mechanism (diagnostics): reactors (waves) per
+ * workgroup, resident waves per CU (occupancy calculator: VGPRs and LDS), LDS bytes per
+ * workgroup (staged tables + one block per reactor). Any pointer may be NULL. */
+int br_mech_launch_info(const br_mech* m, int* rpb, int* waves_per_cu, long long* lds_bytes);
 
 /* host-buffer entry points (copy in/out); arrays are reactor-major */
 int br_rates(br_mech* m, int N, const double* T, const double* p, const double* x /*[N][ng]*/,

@@ -18,11 +18,12 @@ from batchreactor_amd import ensemble  # noqa: E402
 LIB = os.path.join(ROOT, "tests", "golden", "lib")
 case = sys.argv[1] if len(sys.argv) > 1 else "gri"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-gas = {"h2o2": "h2o2.dat", "gri": "grimech.dat", "surf": None}[case]
-surf = "ch4ni.xml" if case == "surf" else None
+gas = {"h2o2": "h2o2.dat", "gri": "grimech.dat", "surf": None, "gas_surf": "grimech.dat"}[case]
+surf = "ch4ni.xml" if case in ("surf", "gas_surf") else None
 SG = "CH4 H2O H2 CO CO2 O2 N2".split()
 pm = pkg.Mechanism.from_files(LIB, gas_mech=gas, surface_mech=surf, gasphase=None if gas else SG)
 eng = pkg.Engine(pm)
+print("launch:", eng.launch_info)
 T, Asv, U0 = ensemble.make_inputs(pm, case, 0, N)
 t0 = time.perf_counter()
 U, st = eng.integrate(T, Asv, U0, 10.0)
