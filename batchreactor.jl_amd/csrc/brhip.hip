@@ -761,10 +761,10 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (
 #define BR_WPE 2
 #endif
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
-// needs ~26 KB of LDS per reactor, so only one workgroup of up to 5 reactors (tables staged once)
-// fits a CU's 160 KB: 5 waves/CU instead of 4 with 1-reactor workgroups (C5 10.7k -> 12.4k/s);
+// needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
+// (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
 // n <= 64 keeps 256-thread workgroups (2 x 4 or 4 x 2 reactors, 8 waves/CU, VGPR-limited)
-__host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 5 : 4; }
+__host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 6 : 4; }
 template <int NMAX>
 __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))) void k_integrate(
     DevMech M, int N, int rpb, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
