@@ -765,8 +765,13 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
 // n <= 64 keeps 256-thread workgroups (2 x 4 or 4 x 2 reactors, 8 waves/CU, VGPR-limited)
 __host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 6 : 4; }
+#ifndef BR_WPE32
+#define BR_WPE32 3   // n <= 32 (surface-only): 3 waves/SIMD, 12 waves/CU (LDS allows it; 130k -> 156k/s)
+#endif
+// minimum waves per SIMD the register allocator must allow, per instance
+__host__ __device__ constexpr int br_wpe(int nmax) { return nmax == 32 ? BR_WPE32 : BR_WPE; }
 template <int NMAX>
-__global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_per_eu(BR_WPE, 8))) void k_integrate(
+__global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_per_eu(br_wpe(NMAX), 8))) void k_integrate(
     DevMech M, int N, int rpb, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
     const double* __restrict__ tfv, KOpts o, double* __restrict__ stats, double* __restrict__ Jws,
     double* __restrict__ trace) {
