@@ -76,7 +76,25 @@ struct Ctl {
 constexpr int CTL_BYTES = (sizeof(Ctl) + 15) / 16 * 16;
 enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, acor, ewt, tempv, y
 // V[vec * VW + component], VW = 64 * CPL components per vector
-__host__ __device__ inline int vec_bytes(int cpl) { return NVEC * WAVE * cpl * 8; }
+// Two components per lane (n = 65..72): the vectors are stored 72 wide, not 128; components
+// 72..127 (lanes 8..63 of the second slot, never active) share one 56-double dump row, so a
+// gas+surface reactor needs 5.7 KB instead of 9.2 KB here (8 reactors per CU instead of 6)
+constexpr int VROW2 = 72;
+__host__ __device__ inline int vec_bytes(int cpl) { return cpl == 2 ? (NVEC * VROW2 + 64) * 8 : NVEC * WAVE * 8; }
+// V[vec * VW + component] accessor (VW = 64 * CPL, the logical row width)
+template <int CPL>
+struct VA {
+    typedef __attribute__((address_space(3))) double LD;
+    LD* p;
+    __device__ __forceinline__ LD& operator[](int i) const {
+        if constexpr (CPL == 1) {
+            return p[i];
+        } else {
+            const int row = i >> 7, c = i & 127;
+            return c < VROW2 ? p[row * VROW2 + c] : p[NVEC * VROW2 + (c & 63)];
+        }
+    }
+};
 typedef __attribute__((address_space(3))) Ctl LCtl;
 typedef __attribute__((address_space(3))) double LDbl;
 
@@ -234,7 +252,7 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
 
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
 template <int CPL>
-__device__ __forceinline__ void cv_rescale(LCtl* C, LDbl* V, int lane) {
+__device__ __forceinline__ void cv_rescale(LCtl* C, VA<CPL> V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     const double eta = ud(C->eta);
@@ -249,7 +267,7 @@ __device__ __forceinline__ void cv_rescale(LCtl* C, LDbl* V, int lane) {
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
 template <int CPL>
-__device__ __forceinline__ void cv_predict(LCtl* C, LDbl* V, int lane) {
+__device__ __forceinline__ void cv_predict(LCtl* C, VA<CPL> V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     double tn = ud(C->tn) + ud(C->h);
@@ -271,7 +289,7 @@ __device__ __forceinline__ void cv_predict(LCtl* C, LDbl* V, int lane) {
     }
 }
 template <int CPL>
-__device__ __forceinline__ void cv_restore(LCtl* C, LDbl* V, int lane) {
+__device__ __forceinline__ void cv_restore(LCtl* C, VA<CPL> V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     C->tn = ud(C->saved_t);
@@ -291,7 +309,7 @@ __device__ __forceinline__ void cv_restore(LCtl* C, LDbl* V, int lane) {
 }
 // cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
 template <int CPL>
-__device__ __forceinline__ void cv_adjust_order(LCtl* C, LDbl* V, int lane, int dq) {
+__device__ __forceinline__ void cv_adjust_order(LCtl* C, VA<CPL> V, int lane, int dq) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     if (q == 2 && dq != 1) return;
@@ -347,7 +365,7 @@ __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, i
 }
 // one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
 template <int CPL>
-__device__ __forceinline__ void begin_attempt(LCtl* C, LDbl* V, int lane, int nflag) {
+__device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL> V, int lane, int nflag) {
     constexpr int VW = 64 * CPL;
     cv_predict<CPL>(C, V, lane);
     cv_set(C);
@@ -365,7 +383,7 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, LDbl* V, int lane, int nf
     FOR_S V[V_Y * VW + CS] = V[CS];   // y = z0
 }
 template <int CPL>
-__device__ __forceinline__ void begin_step(LCtl* C, LDbl* V, int lane, const CtlArgs& a) {
+__device__ __forceinline__ void begin_step(LCtl* C, VA<CPL> V, int lane, const CtlArgs& a) {
     constexpr int VW = 64 * CPL;
 #pragma unroll
     FOR_S {
@@ -389,7 +407,7 @@ __device__ __forceinline__ void begin_step(LCtl* C, LDbl* V, int lane, const Ctl
 // Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
 template <int CPL>
-__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, LDbl* V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
     constexpr int VW = 64 * CPL;
     const CtlArgs a = load_args(C);
     const int n = a.n;
@@ -532,7 +550,7 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
 template <int CPL>
-__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (&delta)[CPL], int lu_fail) {
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double (&delta)[CPL], int lu_fail) {
     constexpr int VW = 64 * CPL;
     const CtlArgs a = load_args(C);
     const int n = a.n;
@@ -764,7 +782,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, LDbl* V, int lane, double (
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
 // n <= 64 keeps 256-thread workgroups (2 x 4 or 4 x 2 reactors, 8 waves/CU, VGPR-limited)
-__host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 6 : 4; }
+__host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 8 : 4; }
 #ifndef BR_WPE32
 #define BR_WPE32 3   // n <= 32 (surface-only): 3 waves/SIMD, 12 waves/CU (LDS allows it; 130k -> 156k/s)
 #endif
@@ -798,7 +816,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const Tab& tb = W.tb;
     const size_t roff = (size_t)(W.rbase - smem_raw);
     LCtl* C = (LCtl*)(smem_raw + roff);
-    LDbl* V = (LDbl*)(smem_raw + roff + CTL_BYTES);
+    const VA<CPL> V{(LDbl*)(smem_raw + roff + CTL_BYTES)};
     const RView& S = W.R;
     const int n = M.n;
     const double T = Tv[rid];
