@@ -47,6 +47,8 @@ typedef struct {
     double A0, b0, E0oR;       /* low-pressure limit (SI) */
     double ta, t3, t1, t2;
     double* eff;               /* [ng], NULL if tb==0 */
+    double fmul, rmul;         /* per-reaction multipliers on the forward / reverse terms
+                                  (1.0; convention-fitting hook for tests, orc_set_rxn_mult) */
 } grxn_t;
 
 typedef struct {
@@ -78,6 +80,9 @@ double orc_molwt(const orc_mech* m, int k) { return m->M[k]; }
 double orc_site_density(const orc_mech* m) { return m->site_density; }
 void orc_initial_coverage(const orc_mech* m, double* th) { for (int i = 0; i < m->ns; ++i) th[i] = m->th0[i]; }
 void orc_set_conv(orc_mech* m, int conv) { m->conv = conv; }
+void orc_set_rxn_mult(orc_mech* m, int i, double fmul, double rmul) {
+    if (i >= 0 && i < m->nrg) { m->gr[i].fmul = fmul; m->gr[i].rmul = rmul; }
+}
 
 /* atomic weights [g/mol]. H/C/O/N fitted to the golden: they reproduce rho0 of
  * test/batch_gas_and_surf/gas_profile.csv row 1 bit-exactly and p(t) on every golden row
@@ -254,6 +259,7 @@ static int load_chemkin(orc_mech* m, const char* path) {
             for (int i = 0; i < nt - 3; ++i) strncat(eq, toks[i], sizeof eq - strlen(eq) - 1);
             if (m->nrg == cap) { cap *= 2; m->gr = (grxn_t*)realloc(m->gr, (size_t)cap * sizeof(grxn_t)); }
             grxn_t* r = &m->gr[m->nrg]; memset(r, 0, sizeof *r);
+            r->fmul = r->rmul = 1.0;
             /* falloff marker "(+M)" */
             char* pm;
             int falloff = 0;
@@ -551,7 +557,8 @@ static void tcache_init(const orc_mech* m, double T, tcache_t* c) {
             for (int e = 0; e < r->nr; ++e) dg += g[r->r[e]];
             for (int e = 0; e < r->nf; ++e) dg -= g[r->f[e]];
             double Kc = exp(-dg) * pow(m->p_std / (R_GAS * T), r->dnu);
-            if ((m->conv & ORC_CONV_KC_UNIT_SLIP) && r->tb != 2) Kc *= pow(1e6, r->dnu);
+            /* GasphaseReactions evaluates rates in mol/cm3 but Kc = Kp (p0/RT)^dnu in mol/m3 */
+            if (m->conv & ORC_CONV_KC_UNIT_SLIP) Kc *= pow(1e6, r->dnu);
             c->kr[i] = c->kf[i] / Kc;
         }
         c->k0[i] = 0; c->fc[i] = 1;
@@ -573,7 +580,7 @@ static void tcache_init(const orc_mech* m, double T, tcache_t* c) {
 static void tcache_free(tcache_t* c) { free(c->kf); }
 
 /* falloff factor fac = Pr/(1+Pr)*F and d(fac)/d[M] */
-static void falloff(const grxn_t* r, const tcache_t* c, int i, double Mc, double* fac, double* dfac) {
+static void falloff(const orc_mech* m, const grxn_t* r, const tcache_t* c, int i, double Mc, double* fac, double* dfac) {
     double kinf = c->kf[i], k0 = c->k0[i];
     double Pr = k0 * Mc / kinf;
     double F = 1.0, g = 0.0;
@@ -581,7 +588,7 @@ static void falloff(const grxn_t* r, const tcache_t* c, int i, double Mc, double
         double Prs = Pr > 1e-300 ? Pr : 1e-300;
         double lfc = log10(c->fc[i]);
         double L = log10(Prs);
-        double cc = -0.4 - 0.67 * lfc, nn = 0.75 - 1.27 * lfc;
+        double cc = ((m->conv & ORC_CONV_TROE_C4) ? -4.0 : -0.4) - 0.67 * lfc, nn = 0.75 - 1.27 * lfc;
         double den = nn - 0.14 * (L + cc);
         double f1 = (L + cc) / den;
         double lF = lfc / (1 + f1 * f1);
@@ -601,15 +608,15 @@ static void gas_rop(const orc_mech* m, const tcache_t* tc, const double* c, doub
         double Pf = 1, Pb = 1;
         for (int e = 0; e < r->nf; ++e) Pf *= c[r->f[e]];
         for (int e = 0; e < r->nr; ++e) Pb *= c[r->r[e]];
-        double D = tc->kf[i] * Pf - tc->kr[i] * Pb;
+        double D = r->fmul * tc->kf[i] * Pf - r->rmul * tc->kr[i] * Pb;
         if (r->tb) {
             double Mc = 0;
             for (int k = 0; k < m->ng; ++k) Mc += r->eff[k] * c[k];
             if (r->tb == 1) D *= Mc;
             else {
-                double fac, dfac; falloff(r, tc, i, Mc, &fac, &dfac);
+                double fac, dfac; falloff(m, r, tc, i, Mc, &fac, &dfac);
                 D *= fac;
-                if (m->conv & ORC_CONV_FALLOFF_XM) D *= Mc;
+                if (m->conv & ORC_CONV_FALLOFF_XM) D *= Mc * 1e-6;   /* [M] in mol/cm3 */
             }
         }
         q[i] = D;
@@ -745,17 +752,18 @@ static void jac_tc(const orc_mech* m, const tcache_t* tc, double Asv, const doub
         double Pf = 1, Pb = 1;
         for (int e = 0; e < r->nf; ++e) Pf *= c[r->f[e]];
         for (int e = 0; e < r->nr; ++e) Pb *= c[r->r[e]];
-        double kf = tc->kf[i], kr = tc->kr[i];
+        double kf = r->fmul * tc->kf[i], kr = r->rmul * tc->kr[i];
         double D = kf * Pf - kr * Pb;
         double pre = 1, coefM = 0, Mc = 0;
         if (r->tb) {
             for (int k = 0; k < ng; ++k) Mc += r->eff[k] * c[k];
             if (r->tb == 1) { pre = Mc; coefM = 1; }
             else {
-                double fac, dfac; falloff(r, tc, i, Mc, &fac, &dfac);
+                double fac, dfac; falloff(m, r, tc, i, Mc, &fac, &dfac);
                 int xm = (m->conv & ORC_CONV_FALLOFF_XM) != 0;
-                pre = fac * (xm ? Mc : 1.0);
-                coefM = dfac * (xm ? Mc : 1.0) + (xm ? fac : 0.0);
+                const double xs = 1e-6;
+                pre = fac * (xm ? Mc * xs : 1.0);
+                coefM = dfac * (xm ? Mc * xs : 1.0) + (xm ? fac * xs : 0.0);
             }
         }
         for (int e = 0; e < r->nf; ++e) {
@@ -1300,8 +1308,25 @@ static void get_dky(const cv_t* cv, double t, double* y) {
     for (int j = cv->q - 1; j >= 0; --j) for (int i = 0; i < cv->n; ++i) y[i] = cv->zn[j][i] + s * y[i];
 }
 
+static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, double tf,
+                          const orc_opts* o, orc_stats* st, orc_step_cb cb, void* user,
+                          int nout, const double* tout, double* yout);
+
 int orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf,
                   const orc_opts* o, orc_stats* st, orc_step_cb cb, void* user) {
+    return integrate_impl(m, T, Asv, u, tf, o, st, cb, user, 0, NULL, NULL);
+}
+
+/* CVode(..., CV_NORMAL) at each output time: the solver steps past tout and interpolates with
+ * CVodeGetDky(tout, 0) (Nordsieck polynomial); the step sequence is the same as without outputs. */
+int orc_integrate_out(const orc_mech* m, double T, double Asv, double* u, double tf, const orc_opts* o,
+                      orc_stats* st, int nout, const double* tout, double* yout) {
+    return integrate_impl(m, T, Asv, u, tf, o, st, NULL, NULL, nout, tout, yout);
+}
+
+static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, double tf,
+                          const orc_opts* o, orc_stats* st, orc_step_cb cb, void* user,
+                          int nout, const double* tout, double* yout) {
     tcache_t tc; tcache_init(m, T, &tc);
     cv_t cvs; cv_t* cv = &cvs; memset(cv, 0, sizeof *cv);
     int n = m->ng + m->ns;
@@ -1344,6 +1369,8 @@ int orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf,
     for (int i = 0; i < n; ++i) uscale += fabs(u[i]);
     int status = 0;
     long nstloc = 0;
+    int iout = 0;
+    while (iout < nout && tout[iout] <= 0.0) { memcpy(yout + (size_t)iout * n, u, sizeof(double) * (size_t)n); ++iout; }
     for (;;) {
         if (cv->nst > 0) set_ewt(cv, cv->zn[0]);
         if (nstloc >= mxstep) { status = -1; break; }
@@ -1355,6 +1382,7 @@ int orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf,
             for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(cv->zn[0][i]));
             if (!(mx <= ufac * uscale)) { status = -7; break; }
         }
+        while (iout < nout && tout[iout] <= cv->tn) { get_dky(cv, tout[iout], yout + (size_t)iout * n); ++iout; }
         double troundoff = FUZZ_FACTOR * cv->uround * (fabs(cv->tn) + fabs(cv->h));
         if (fabs(cv->tn - cv->tstop) <= troundoff) {
             get_dky(cv, cv->tstop, u);

@@ -30,10 +30,19 @@
 extern "C" {
 #endif
 
-/* convention switches (bitmask); 0 = textbook CHEMKIN-II + current reference code */
-#define ORC_CONV_KC_UNIT_SLIP   1  /* Kc *= (1e6)^dnu for non-falloff reversible reactions */
-#define ORC_CONV_FALLOFF_XM     2  /* falloff net rate *= [M]                               */
+/* convention switches (bitmask); 0 = textbook CHEMKIN-II (SI throughout).
+ * ORC_CONV_REFERENCE = the conventions of the GasphaseReactions version that produced the
+ * reference's golden (test/batch_gas_and_surf/gas_profile.csv), identified in round 2 from the
+ * golden's first 40 accepted steps (tests/test_oracle.py::test_golden_early_rows_all_species):
+ *   KC_UNIT_SLIP  rates in mol/cm3 but Kc = exp(-dG/RT) (p0/RT)^dnu in mol/m3, i.e. in SI terms
+ *                 Kc *= (1e6)^dnu for every reversible reaction;
+ *   FALLOFF_XM    (+M) falloff rates are also multiplied by [M] (in mol/cm3 = 1e-6 [M]_SI);
+ *   TROE_C4       Troe c = -4.0 - 0.67 log10(Fcent) (instead of -0.4). */
+#define ORC_CONV_KC_UNIT_SLIP   1
+#define ORC_CONV_FALLOFF_XM     2
 #define ORC_CONV_DOC_COVG       4  /* no Asv on dtheta/dt (docs sample predates :345)          */
+#define ORC_CONV_TROE_C4       16
+#define ORC_CONV_REFERENCE     (ORC_CONV_KC_UNIT_SLIP | ORC_CONV_FALLOFF_XM | ORC_CONV_TROE_C4)
 
 typedef struct orc_mech orc_mech;
 
@@ -74,6 +83,8 @@ double orc_molwt(const orc_mech* m, int k);
 double orc_site_density(const orc_mech* m);               /* mol/cm2 */
 void   orc_initial_coverage(const orc_mech* m, double* th);
 void   orc_set_conv(orc_mech* m, int conv);
+/* test hook: multiply gas reaction i's forward / reverse terms (default 1.0) */
+void   orc_set_rxn_mult(orc_mech* m, int i, double fmul, double rmul);
 
 /* rho_k from mole fractions (src/BatchReactor.jl:224-232 / IdealGas.density) */
 void orc_initial_state(const orc_mech* m, double T, double p, const double* x, double* u);
@@ -91,6 +102,9 @@ void orc_jac(const orc_mech* m, double T, double Asv, const double* u, double* J
 /* integrate one reactor 0 -> tf; u is in/out */
 int  orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf,
                    const orc_opts* o, orc_stats* st, orc_step_cb cb, void* user);
+/* same, plus the state at nout ascending output times (CV_NORMAL + CVodeGetDky); yout[nout][n] */
+int  orc_integrate_out(const orc_mech* m, double T, double Asv, double* u, double tf, const orc_opts* o,
+                       orc_stats* st, int nout, const double* tout, double* yout);
 /* ensemble (OpenMP over reactors): u[N][n] row per reactor */
 int  orc_integrate_batch(const orc_mech* m, int N, const double* T, const double* Asv,
                          double* u, const double* tf, const orc_opts* o, orc_stats* st,

@@ -16,6 +16,8 @@ LIB = os.path.join(HERE, "liboracle.so")
 CONV_KC_UNIT_SLIP = 1
 CONV_FALLOFF_XM = 2
 CONV_DOC_COVG = 4
+CONV_TROE_C4 = 16
+CONV_REFERENCE = CONV_KC_UNIT_SLIP | CONV_FALLOFF_XM | CONV_TROE_C4   # GasphaseReactions (golden)
 
 
 class Opts(C.Structure):
@@ -65,6 +67,7 @@ def lib():
         L.orc_site_density.restype = C.c_double
         L.orc_initial_coverage.argtypes = [C.c_void_p, dp]
         L.orc_set_conv.argtypes = [C.c_void_p, C.c_int]
+        L.orc_set_rxn_mult.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double]
         L.orc_initial_state.argtypes = [C.c_void_p, C.c_double, C.c_double, dp, dp]
         L.orc_rates.argtypes = [C.c_void_p, C.c_double, C.c_double, dp, dp, dp, dp]
         L.orc_rop.argtypes = [C.c_void_p, C.c_double, C.c_double, dp, dp, dp, dp]
@@ -73,6 +76,9 @@ def lib():
         L.orc_integrate.argtypes = [C.c_void_p, C.c_double, C.c_double, dp, C.c_double,
                                     C.POINTER(Opts), C.POINTER(Stats), STEP_CB, C.c_void_p]
         L.orc_integrate.restype = C.c_int
+        L.orc_integrate_out.argtypes = [C.c_void_p, C.c_double, C.c_double, dp, C.c_double, C.POINTER(Opts),
+                                        C.POINTER(Stats), C.c_int, dp, dp]
+        L.orc_integrate_out.restype = C.c_int
         L.orc_integrate_batch.argtypes = [C.c_void_p, C.c_int, dp, dp, dp, dp, C.POINTER(Opts),
                                           C.POINTER(Stats), C.c_int]
         L.orc_integrate_batch.restype = C.c_int
@@ -115,6 +121,9 @@ class Mech:
 
     def set_conv(self, conv):
         lib().orc_set_conv(self.h, conv)
+
+    def set_rxn_mult(self, i, fmul, rmul):
+        lib().orc_set_rxn_mult(self.h, i, fmul, rmul)
 
     def initial_state(self, T, p, x):
         x = np.ascontiguousarray(x, dtype=np.float64)
@@ -168,6 +177,16 @@ class Mech:
         fcb = STEP_CB(cb) if record else STEP_CB()
         r = lib().orc_integrate(self.h, T, Asv, _p(u), tf, C.byref(o), C.byref(st), fcb, None)
         return u, st.asdict(), rows
+
+    def integrate_out(self, T, Asv, u0, tf, tout, rtol=1e-6, atol=1e-10, analytic_jac=False, max_steps=100000):
+        """State at the output times `tout` (ascending), CVODE CV_NORMAL + CVodeGetDky semantics."""
+        u = np.array(u0, dtype=np.float64)
+        tout = np.ascontiguousarray(tout, dtype=np.float64)
+        Y = np.zeros((len(tout), self.n))
+        o = Opts(rtol, atol, int(analytic_jac), max_steps, 0.0)
+        st = Stats()
+        lib().orc_integrate_out(self.h, T, Asv, _p(u), tf, C.byref(o), C.byref(st), len(tout), _p(tout), _p(Y))
+        return u, st.asdict(), Y
 
     def integrate_batch(self, T, Asv, U0, tf, rtol=1e-6, atol=1e-10, analytic_jac=True, nthreads=0):
         N = len(T)
