@@ -27,10 +27,11 @@ class MechDesc(C.Structure):
 
 class Opts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("max_steps", C.c_int), ("device", C.c_int),
-                ("hmax", C.c_double), ("trace_cap", C.c_int), ("unstable_factor", C.c_double)]
+                ("hmax", C.c_double), ("trace_cap", C.c_int), ("unstable_factor", C.c_double),
+                ("ignition_species", C.c_int), ("nout", C.c_int), ("tout", dp), ("yout", dp)]
 
 
-NSTAT = 16
+NSTAT = 20
 
 
 EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info", "br_mech_engine", "br_mech_launch_info",

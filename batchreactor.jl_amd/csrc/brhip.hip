@@ -41,6 +41,10 @@ enum { NO_FAILURES = 0, FAIL_BAD_J = 1, FAIL_OTHER = 2 };
 struct KOpts {
     double rtol, atol, hmax_inv, ufac;
     int max_steps, trace_cap;
+    int ign;                  // gas species index of the ignition marker (-1: not tracked)
+    int nout;                 // dense output: tout[nout] (device), yout[N][nout][n] (device)
+    const double* tout;
+    double* yout;
     int defer_steps;          // k_lane: hand a reactor still running after this many steps to the
                               // wavefront engine (restart from u0); >= max_steps disables
     const int* rid_list;      // k_integrate: integrate reactors rid_list[0 .. min(*rid_count, N)) only
@@ -68,10 +72,15 @@ struct Ctl {
     int nst, nfe, nsetups, nje, nni, ncfn, netf, nstlp, nstlj;
     int ncf, nef, nstloc, status, m_it, convfail, count1, phase;
     int callSetup, jbad, jcur_nls, hnewOK, newj;
+    // ignition marker (max dX_ign/dt over accepted steps) and dense-output cursor
+    double ign_x, ign_t, ign_rate, t_ign;
+    int iout;
     // per-launch constants (here rather than in registers: they are read once per step)
     double a_rtol, a_atol, a_hmax_inv, a_ufac;
     double* a_trace;
-    int a_max_steps, a_trace_cap, a_rid, a_n;
+    const double* a_tout;
+    double* a_yout;
+    int a_max_steps, a_trace_cap, a_rid, a_n, a_ign, a_nout;
 };
 constexpr int CTL_BYTES = (sizeof(Ctl) + 15) / 16 * 16;
 enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, acor, ewt, tempv, y
@@ -158,18 +167,70 @@ __device__ __forceinline__ double wrms_l(const double (&v)[CPL], const double (&
 struct CtlArgs {   // per-launch constants the controller needs, read (uniform) from the LDS controller
     double rtol, atol, hmax_inv, ufac;
     double* trace;
-    int max_steps, trace_cap, rid, n;
+    const double* tout;
+    double* yout;
+    int max_steps, trace_cap, rid, n, ign, nout;
 };
+// uniform 64-bit pointer from the LDS controller
+template <class P>
+__device__ __forceinline__ P ld_ptr(const __attribute__((address_space(3))) P& f) {
+    const volatile __attribute__((address_space(3))) unsigned long long& tp =
+        *reinterpret_cast<const volatile __attribute__((address_space(3))) unsigned long long*>(&f);
+    const unsigned long long tv = tp;
+    const unsigned lo = (unsigned)uni((int)(tv & 0xffffffffull)), hi = (unsigned)uni((int)(tv >> 32));
+    return reinterpret_cast<P>(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ CtlArgs load_args(LCtl* C) {
     CtlArgs a;
     a.rtol = ud(C->a_rtol); a.atol = ud(C->a_atol); a.hmax_inv = ud(C->a_hmax_inv); a.ufac = ud(C->a_ufac);
-    const volatile __attribute__((address_space(3))) unsigned long long& tp =
-        *reinterpret_cast<volatile __attribute__((address_space(3))) unsigned long long*>(&C->a_trace);
-    const unsigned long long tv = tp;
-    const unsigned lo = (unsigned)uni((int)(tv & 0xffffffffull)), hi = (unsigned)uni((int)(tv >> 32));
-    a.trace = reinterpret_cast<double*>(((unsigned long long)hi << 32) | lo);
+    a.trace = ld_ptr(C->a_trace);
+    a.tout = ld_ptr(C->a_tout);
+    a.yout = ld_ptr(C->a_yout);
     a.max_steps = ui(C->a_max_steps); a.trace_cap = ui(C->a_trace_cap); a.rid = ui(C->a_rid); a.n = ui(C->a_n);
+    a.ign = ui(C->a_ign); a.nout = ui(C->a_nout);
     return a;
+}
+
+// mole fraction of gas species k in state v (components lane + 64 s): (v_k/M_k) / sum_j v_j/M_j
+template <int CPL>
+__device__ __forceinline__ double mole_frac_of(const double (&v)[CPL], int lane, int k) {
+    const double* mw = reinterpret_cast<const double*>(br_lds);   // staged molwt[] (image offset 0)
+    const int ng = MF(ng);
+    double g = 0.0, xk = 0.0;
+#pragma unroll
+    FOR_S if (CS < ng) { const double c = v[s] / mw[CS]; g += c; xk = (CS == k) ? c : xk; }
+    return wave_sum(xk) / wave_sum(g);
+}
+// ignition marker after an accepted step to (tn, v): midpoint of the step with the largest dX/dt
+template <int CPL>
+__device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int lane, double tn, const double (&v)[CPL]) {
+    const double x = uni(mole_frac_of<CPL>(v, lane, a.ign));
+    const double t0 = ud(C->ign_t);
+    const double r = (x - ud(C->ign_x)) / (tn - t0);
+    if (r > ud(C->ign_rate)) { C->ign_rate = r; C->t_ign = 0.5 * (t0 + tn); }
+    C->ign_x = x; C->ign_t = tn;
+}
+// dense output (CVode CV_NORMAL): every tout in (t_{n-1}, t_n] from the Nordsieck array of the step
+// just completed, y(t) = sum_j z_j ((t - tn)/h)^j (CVodeGetDky, k = 0)
+template <int CPL>
+__device__ __forceinline__ void dense_output(LCtl* C, VA<CPL> V, const CtlArgs& a, int lane, double tn, double h, int q,
+                                             double tlim) {
+    constexpr int VW = 64 * CPL;
+    int io = ui(C->iout);
+    while (io < a.nout) {
+        const double t = uni(a.tout[io]);
+        if (!(t <= tlim)) break;
+        const double sk = (t - tn) / h;
+        double* row = a.yout + ((size_t)a.rid * a.nout + io) * a.n;
+#pragma unroll
+        FOR_S {
+            double yv = V[q * VW + CS];
+            for (int j = q - 1; j >= 0; --j) yv = V[j * VW + CS] + sk * yv;
+            if (CS < a.n) row[CS] = yv;
+        }
+        ++io;
+    }
+    C->iout = io;
 }
 
 // 1.0 / j for the small integers of the BDF coefficient formulas (exactly the rounded quotient)
@@ -735,17 +796,20 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
         FOR_S yl[s] = V[V_Y * VW + CS];                     // the last RHS was evaluated at y
         trace_row<CPL>(C, a, lane, nst, tn, z0, yl);
     }
-    if (a.ufac > 0.0) {                                      // runaway state (br_opts.unstable_factor)
+    if (a.ign >= 0) track_ignition<CPL>(C, a, lane, tn, z0);
+    if (a.nout) dense_output<CPL>(C, V, a, lane, tn, h, q, tn);
+    {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor)
         double zm = 0.0;
 #pragma unroll
-        FOR_S if (CS < n) zm = fmax(zm, fabs(z0[s]));
+        FOR_S if (CS < n) { const double a = fabs(z0[s]); zm = fmax(zm, a == a ? a : INFINITY); }
         const double mx = uni(wave_max(zm));
-        if (!(mx <= ud(C->ulimit))) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
+        if (!(mx < INFINITY) || mx > ud(C->ulimit)) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
     }
     // CVode ONE_STEP + tstop handling
     const double tstop = ud(C->tstop);
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
     if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
+        if (a.nout) dense_output<CPL>(C, V, a, lane, tn, h, q, tstop);
         const double sk = (tstop - tn) / h;
 #pragma unroll
         FOR_S {
@@ -827,6 +891,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     double* jscr = LUsave + lu_ws_doubles(NMAX);
     C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
     C->a_max_steps = o.max_steps; C->a_trace_cap = o.trace_cap; C->a_trace = trace; C->a_rid = rid; C->a_n = n;
+    C->a_ign = o.ign; C->a_nout = o.nout; C->a_tout = o.tout; C->a_yout = o.yout;
 
     init_tconst<CPL>(M, tb, S, T, lane);
 
@@ -853,12 +918,23 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     C->delp = 0.0; C->hprime = 0.0; C->hscale = 0.0; C->eta = 1.0; C->etamax = ETAMX1; C->acnrm = 0.0;
     C->saved_tq5 = 0.0; C->saved_t = 0.0; C->tol = 0.0; C->hg = 0.0; C->hub = 0.0; C->hlb = 0.0; C->hnew = 0.0;
     C->tstop = tfv[rid];
-    C->ulimit = o.ufac * uni(wave_sum(su));
+    C->ulimit = o.ufac > 0.0 ? o.ufac * uni(wave_sum(su)) : INFINITY;
     C->q = 1; C->qprime = 1; C->L = 2; C->qwait = 2;
     C->nst = 0; C->nfe = 0; C->nsetups = 0; C->nje = 0; C->nni = 0; C->ncfn = 0; C->netf = 0; C->nstlp = 0;
     C->nstlj = 0; C->ncf = 0; C->nef = 0; C->nstloc = 0; C->status = 0; C->m_it = 0; C->convfail = 0;
     C->count1 = 0; C->phase = PH_F0; C->callSetup = 0; C->jbad = 0; C->jcur_nls = 0; C->hnewOK = 0; C->newj = 0;
     C->p_last = 0.0;
+    C->iout = 0; C->ign_t = 0.0; C->ign_rate = -INFINITY; C->t_ign = NAN; C->ign_x = 0.0;
+    if (o.ign >= 0) C->ign_x = uni(mole_frac_of<CPL>(u0, lane, o.ign));
+    if (o.nout) {                                           // outputs at t <= 0: the initial state
+        int io = 0;
+        while (io < o.nout && !(o.tout[io] > 0.0)) {
+#pragma unroll
+            FOR_S if (CS < n) o.yout[((size_t)rid * o.nout + io) * n + CS] = u0[s];
+            ++io;
+        }
+        C->iout = io;
+    }
 
 #if BR_PHASE_CLOCKS
     unsigned long long cyc_rhs = 0, cyc_jac = 0, cyc_lu = 0, cyc_sol = 0, cyc_ctl = 0;
@@ -939,6 +1015,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         st[9] = st[10] = st[11] = st[12] = st[14] = st[15] = 0.0;
 #endif
         st[13] = ud(C->tn);
+        st[16] = o.ign >= 0 ? ud(C->t_ign) : NAN; st[17] = o.ign >= 0 ? ud(C->ign_rate) : NAN;
+        st[18] = st[19] = 0.0;
     }
     }   // next reactor
 }
@@ -1191,7 +1269,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
             delete m; return fail(BR_ERR_UNSUPPORTED, "reaction touches more than 6 species");
         }
         for (int c = 0; c < 3; ++c) gpar[4 * (size_t)i + c] = d->g_arr[r * 3 + c];
-        gpar[4 * (size_t)i + 3] = ((d->conv & BR_CONV_KC_UNIT_SLIP) && tb != 2) ? std::pow(1e6, (double)(nr - nf)) : 1.0;
+        gpar[4 * (size_t)i + 3] = (d->conv & BR_CONV_KC_UNIT_SLIP) ? std::pow(1e6, (double)(nr - nf)) : 1.0;
         gdnu[i] = nr - nf;
         int troe = 0, fo = 0, tbidx = 0;
         if (tb) {   // third-body efficiency set (deduplicated: GRI's 41 reactions use 10 sets)
@@ -1501,7 +1579,11 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.max_steps = (opts && opts->max_steps > 0) ? opts->max_steps : 100000;
     o.hmax_inv = (opts && opts->hmax > 0) ? 1.0 / opts->hmax : 0.0;
     o.trace_cap = (opts && trace) ? opts->trace_cap : 0;
-    o.ufac = (opts && opts->unstable_factor != 0.0) ? opts->unstable_factor : 10.0;
+    o.ufac = opts ? opts->unstable_factor : 0.0;          // <= 0: NaN check only (SciML default)
+    o.ign = (opts && opts->ignition_species > 0 && opts->ignition_species <= m->ng) ? opts->ignition_species - 1 : -1;
+    o.nout = (opts && opts->nout > 0 && opts->tout && opts->yout) ? opts->nout : 0;
+    o.tout = o.nout ? opts->tout : nullptr;
+    o.yout = o.nout ? opts->yout : nullptr;
     o.defer_steps = o.max_steps;
     o.rid_list = nullptr;
     o.rid_count = nullptr;
@@ -1615,7 +1697,9 @@ static int integrate_host(br_mech* m, int N, const double* T, const double* Asv,
     const int cap = (trace && opts) ? opts->trace_cap : 0;
     if (trace && cap <= 0) return fail(BR_ERR_INPUT, "trace_cap must be > 0");
     const size_t ntr = trace ? (size_t)N * (cap + 1) * (2 * n + 4) : 0;
-    const size_t nd = (size_t)N * (3 + n + BR_NSTAT) + ntr;
+    const int nout = (opts && opts->nout > 0 && opts->tout && opts->yout) ? opts->nout : 0;
+    const size_t nyo = (size_t)N * nout * n;
+    const size_t nd = (size_t)N * (3 + n + BR_NSTAT) + ntr + nout + nyo;
     int rc = ensure_ws(m, nd * sizeof(double));
     if (rc) return rc;
     double* dT = (double*)m->ws;
@@ -1624,17 +1708,31 @@ static int integrate_host(br_mech* m, int N, const double* T, const double* Asv,
     double* du_ = dtf + N;
     double* dst = du_ + (size_t)N * n;
     double* dtr = dst + (size_t)N * BR_NSTAT;
+    double* dto = dtr + ntr;
+    double* dyo = dto + nout;
+    br_opts od;
+    if (opts) od = *opts;
+    if (nout) {
+        for (int i = 1; i < nout; ++i)
+            if (!(opts->tout[i] >= opts->tout[i - 1])) return fail(BR_ERR_INPUT, "tout must be ascending");
+        HIPCHK(hipMemcpy(dto, opts->tout, nout * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dyo, opts->yout, nyo * sizeof(double), hipMemcpyHostToDevice));
+        od.tout = dto;
+        od.yout = dyo;
+    }
     HIPCHK(hipMemcpy(dT, T, N * sizeof(double), hipMemcpyHostToDevice));
     if (Asv) HIPCHK(hipMemcpy(dA, Asv, N * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dtf, tf, N * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(du_, u, (size_t)N * n * sizeof(double), hipMemcpyHostToDevice));
     if (trace) HIPCHK(hipMemset(dtr, 0, ntr * sizeof(double)));
-    rc = integrate_dev(m, N, dT, Asv ? dA : nullptr, du_, dtf, opts, (br_stats*)dst, nullptr, trace ? dtr : nullptr);
+    rc = integrate_dev(m, N, dT, Asv ? dA : nullptr, du_, dtf, opts ? &od : nullptr, (br_stats*)dst, nullptr,
+                       trace ? dtr : nullptr);
     if (rc) return rc;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(u, du_, (size_t)N * n * sizeof(double), hipMemcpyDeviceToHost));
     if (stats) HIPCHK(hipMemcpy(stats, dst, (size_t)N * BR_NSTAT * sizeof(double), hipMemcpyDeviceToHost));
     if (trace) HIPCHK(hipMemcpy(trace, dtr, ntr * sizeof(double), hipMemcpyDeviceToHost));
+    if (nout) HIPCHK(hipMemcpy(opts->yout, dyo, nyo * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -287,7 +287,7 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
             }
             const double lfc = log10(fcv);
             fo[1] = lfc;
-            fo[2] = -0.4 - 0.67 * lfc;
+            fo[2] = ((MF(conv) & BR_CONV_TROE_C4) ? -4.0 : -0.4) - 0.67 * lfc;
             fo[3] = 0.75 - 1.27 * lfc;
         }
     }
@@ -385,7 +385,7 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
                 double fac, dfac;
                 falloff<false>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, k.x, Mc, fac, dfac);
                 D *= fac;
-                if (xm) D *= Mc;
+                if (xm) D *= Mc * 1e-6;                                // [M] in mol/cm3
             }
         }
         return D;
@@ -530,8 +530,8 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
             else {
                 double fac, dfac;
                 falloff<true>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, kf, Mc, fac, dfac);
-                pre = fac * (xm ? Mc : 1.0);
-                coefM = dfac * (xm ? Mc : 1.0) + (xm ? fac : 0.0);
+                pre = fac * (xm ? Mc * 1e-6 : 1.0);
+                coefM = dfac * (xm ? Mc * 1e-6 : 1.0) + (xm ? fac * 1e-6 : 0.0);
             }
         }
         jscr[2 * r] = pre;

@@ -126,7 +126,20 @@ struct LCV {
     int q, qprime, L, qwait, nst, nfe, nsetups, nje, nni, ncfn, netf, nstlp, nstlj;
     int ncf, nef, nstloc, status, m_it, convfail, count1, phase, callSetup, jbad, jcur_nls, hnewOK, jcol;
     int pend, pflag;   // deferred step/attempt start (one call site in the kernel): PEND_*, nflag
+    double ign_x, ign_t, ign_rate, t_ign;   // ignition marker (max dX_ign/dt over accepted steps)
+    int iout, rid;                          // dense-output cursor, reactor index
 };
+
+// mole fraction of gas species k (gas-only mechanisms: n = ng) in the lane's state v
+template <int NM>
+__device__ __forceinline__ double l_mole_frac(const double (&v)[NM], int n, int k) {
+    const CF64* mw = (const CF64*)MF(img);                      // molwt[] at image offset 0
+    double g = 0.0, xk = 0.0;
+#pragma unroll
+    for (int i = 0; i < NM; ++i)
+        if (i < n) { const double cc = v[i] / mw[i]; g += cc; xk = (i == k) ? cc : xk; }
+    return xk / g;
+}
 
 // x^(1/L) for the order-dependent step ratios (pow(x, 1.0/L) in CVODE): fp32 estimate of the
 // exponent with the binary exponent split off (any fp64 x > 0), then two fp64 Newton steps
@@ -677,11 +690,35 @@ __device__ __forceinline__ int l_post_solve(LCV& c, ZH<NM>& z, double (&acor)[NM
     for (int i = 0; i < NM; ++i) acor[i] *= c.tq[2];
     c.nstloc += 1;
     c.eta = eta; c.hprime = hprime; c.qprime = qprime;
-    if (o.ufac > 0.0) {                          // runaway state (br_opts.unstable_factor)
+    if (o.ign >= 0) {                            // ignition marker (midpoint of the steepest step)
+        const double x = l_mole_frac<NM>(z.z0, n, o.ign);
+        const double r = (x - c.ign_x) / (c.tn - c.ign_t);
+        if (r > c.ign_rate) { c.ign_rate = r; c.t_ign = 0.5 * (c.ign_t + c.tn); }
+        c.ign_x = x; c.ign_t = c.tn;
+    }
+    const double tlim = fabs(c.tn - c.tstop) <= FUZZ * UROUND * (fabs(c.tn) + fabs(h)) ? c.tstop : c.tn;
+    while (c.iout < o.nout && o.tout[c.iout] <= tlim) {   // dense output (CVodeGetDky, CV_NORMAL)
+        const double sk = (o.tout[c.iout] - c.tn) / h;
+        double zq[NM], yo[NM];
+        z.row(q, zq);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) yo[i] = zq[i];
+#pragma unroll
+        for (int j = QMAX - 1; j >= 0; --j)
+            if (j <= q - 1) {
+#pragma unroll
+                for (int i = 0; i < NM; ++i) yo[i] = z.get(j, i) + sk * yo[i];
+            }
+        double* row = o.yout + ((size_t)c.rid * o.nout + c.iout) * n;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) if (i < n) row[i] = yo[i];
+        c.iout += 1;
+    }
+    {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor)
         double zm = 0.0;
 #pragma unroll
-        for (int i = 0; i < NM; ++i) zm = fmax(zm, fabs(z.z0[i]));
-        if (!(zm <= c.ulimit)) { c.status = BR_ERR_UNSTABLE; return A_DONE; }
+        for (int i = 0; i < NM; ++i) { const double a = fabs(z.z0[i]); zm = fmax(zm, a == a ? a : INFINITY); }
+        if (!(zm < INFINITY) || zm > c.ulimit) { c.status = BR_ERR_UNSTABLE; return A_DONE; }
     }
     const double tn = c.tn;
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
@@ -844,7 +881,7 @@ __device__ __forceinline__ void lane_tconst(const LaneLay& LL, double* Lp, const
             }
             const double lfc = log10(fcv);
             G.st(LL.g_fod + 4 * fi + 1, lfc);
-            G.st(LL.g_fod + 4 * fi + 2, -0.4 - 0.67 * lfc);
+            G.st(LL.g_fod + 4 * fi + 2, ((MF(conv) & BR_CONV_TROE_C4) ? -4.0 : -0.4) - 0.67 * lfc);
             G.st(LL.g_fod + 4 * fi + 3, 0.75 - 1.27 * lfc);
         }
     }
@@ -931,7 +968,7 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
                     F = pow(10.0, lfc / (1 + f1 * f1));
                 }
                 D *= Pr / (1 + Pr) * F;
-                if (xm) D *= Mc;
+                if (xm) D *= Mc * 1e-6;                         // [M] in mol/cm3
             }
         }
         const int cnt = (s1 >> 16) & 255;
@@ -1010,12 +1047,20 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
                 c.tn = 0.0; c.h = 0.0; c.hprime = 0.0; c.hscale = 0.0; c.eta = 1.0; c.etamax = ETAMX1;
                 c.rl1 = 0.0; c.gamma = 0.0; c.gammap = 0.0; c.gamrat = 1.0; c.crate = 1.0; c.delp = 0.0;
                 c.acnrm = 0.0; c.saved_tq5 = 0.0; c.saved_t = 0.0; c.tol = 0.0; c.hg = 0.0; c.hub = 0.0;
-                c.hlb = 0.0; c.tstop = tfv[rid]; c.ulimit = o.ufac * su; c.minInc = 0.0;
+                c.hlb = 0.0; c.tstop = tfv[rid]; c.ulimit = o.ufac > 0.0 ? o.ufac * su : INFINITY; c.minInc = 0.0;
                 c.q = 1; c.qprime = 1; c.L = 2; c.qwait = 2;
                 c.nst = 0; c.nfe = 0; c.nsetups = 0; c.nje = 0; c.nni = 0; c.ncfn = 0; c.netf = 0;
                 c.nstlp = 0; c.nstlj = 0; c.ncf = 0; c.nef = 0; c.nstloc = 0; c.status = 0; c.m_it = 0;
                 c.convfail = 0; c.count1 = 0; c.phase = PH_F0; c.callSetup = 0; c.jbad = 0; c.jcur_nls = 0;
                 c.hnewOK = 0; c.jcol = 0; c.pend = PEND_NONE; c.pflag = 0;
+                c.rid = rid; c.iout = 0; c.ign_t = 0.0; c.ign_rate = -INFINITY; c.t_ign = NAN;
+                c.ign_x = o.ign >= 0 ? l_mole_frac<NM>(y, n, o.ign) : 0.0;
+                while (c.iout < o.nout && !(o.tout[c.iout] > 0.0)) {   // outputs at t <= 0: u0
+                    double* row = o.yout + ((size_t)rid * o.nout + c.iout) * n;
+#pragma unroll
+                    for (int i = 0; i < NM; ++i) if (i < n) row[i] = y[i];
+                    c.iout += 1;
+                }
             } else {
                 drained = true;
             }
@@ -1097,6 +1142,8 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
                 st[9] = st[10] = st[11] = st[12] = st[14] = st[15] = 0.0;
 #endif
                 st[13] = c.tn;
+                st[16] = o.ign >= 0 ? c.t_ign : NAN; st[17] = o.ign >= 0 ? c.ign_rate : NAN;
+                st[18] = st[19] = 0.0;
             }
             has = false;
         }

@@ -18,7 +18,9 @@ from . import _lib
 from .mechanism import Mechanism
 
 STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status", "cyc_total", "cyc_rhs",
-               "cyc_jac", "cyc_lu", "cyc_sol", "t_end", "cyc_ctl", "cyc_clk")
+               "cyc_jac", "cyc_lu", "cyc_sol", "t_end", "cyc_ctl", "cyc_clk", "t_ign", "ign_rate", "reserved0",
+               "reserved1")
+IGNITION_MARKER = "OH"   # the reference golden's ignition marker: max dX_OH/dt
 
 
 class Engine:
@@ -51,6 +53,8 @@ class Engine:
         _lib.check(L.br_mech_create(C.byref(desc), device, C.byref(h)))
         self.h = h
         self.n, self.ng, self.ns = mech.n, mech.ng, mech.ns
+        # 1-based br_opts.ignition_species (0: the mechanism has no OH, t_ign not tracked)
+        self.ign1 = mech.gas_species.index(IGNITION_MARKER) + 1 if IGNITION_MARKER in mech.gas_species else 0
         self.nmax = 16 if self.n <= 16 else 32 if self.n <= 32 else 56 if self.n <= 56 else 64 if self.n <= 64 else 72   # kernel tile
 
     @property
@@ -114,15 +118,25 @@ class Engine:
         _lib.check(_lib.lib().br_jacobian(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(J)))
         return J
 
-    def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000, trace_cap=0):
+    def _opts(self, rtol, atol, max_steps, trace_cap=0, unstable_factor=0.0, tout=None, yout=None):
+        nout = 0 if tout is None else len(tout)
+        return _lib.Opts(rtol, atol, max_steps, self.device, 0.0, trace_cap, unstable_factor, self.ign1, nout,
+                         _lib.dptr(tout) if nout else None, _lib.dptr(yout) if nout else None)
+
+    def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000, trace_cap=0, tout=None,
+                  unstable_factor=0.0):
         """Integrate N reactors 0 -> tf. With trace_cap > 0 also returns the per-step rows
         trace[N, trace_cap+1, 2n+4] = (t, h, q, p_last, u[n], y_last[n]): u the accepted state, y_last
-        and p_last the state and pressure of the step's last RHS evaluation (save_data semantics)."""
+        and p_last the state and pressure of the step's last RHS evaluation (save_data semantics).
+        With tout (ascending output times) the stats dict also carries "yout" [N, nout, n], the
+        states at those times (CVODE CV_NORMAL output, the step sequence is unchanged)."""
         u = np.array(np.atleast_2d(u0), dtype=np.float64, order="C")
         N = u.shape[0]
         T, A, tf = self._arr(T, N), self._arr(Asv, N), self._arr(tf, N)
         st = np.zeros((N, _lib.NSTAT))
-        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0, trace_cap)
+        to = None if tout is None else np.ascontiguousarray(tout, dtype=np.float64)
+        yo = None if tout is None else np.zeros((N, len(to), self.n))
+        o = self._opts(rtol, atol, max_steps, trace_cap, unstable_factor, to, yo)
         L = _lib.lib()
         if trace_cap > 0:
             tr = np.zeros((N, trace_cap + 1, 2 * self.n + 4))
@@ -133,12 +147,14 @@ class Engine:
             _lib.check(L.br_integrate(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(tf),
                                       C.byref(o), _lib.dptr(st)))
         stats = {k: st[:, i] for i, k in enumerate(STAT_FIELDS)}
+        if yo is not None:
+            stats["yout"] = yo
         return (u, stats, tr) if trace_cap > 0 else (u, stats)
 
     def integrate_device(self, T_ptr, Asv_ptr, u_ptr, tf_ptr, stats_ptr, N, stream_ptr=None, rtol=1e-6,
                          atol=1e-10, max_steps=100000):
         """Device-resident variant: raw device pointers (e.g. torch tensor data_ptr())."""
-        o = _lib.Opts(rtol, atol, max_steps, self.device, 0.0, 0)
+        o = self._opts(rtol, atol, max_steps)
         _lib.check(_lib.lib().br_integrate_dev(self.h, N, C.c_void_p(T_ptr), C.c_void_p(Asv_ptr),
                                                C.c_void_p(u_ptr), C.c_void_p(tf_ptr), C.byref(o),
                                                C.c_void_p(stats_ptr), C.c_void_p(stream_ptr or 0)))

@@ -30,9 +30,15 @@ ATOMIC_WEIGHTS = {
     "NE": 20.1797, "S": 32.065, "CL": 35.453, "F": 18.9984, "E": 5.48579909e-4,
 }
 
+# Gas-kinetics convention switches (include/brhip.h BR_CONV_*). 0 = textbook CHEMKIN-II in SI.
+# CONV_REFERENCE = what the reference's GasphaseReactions does (identified from its golden output,
+# DESIGN.md section 1): rates in mol/cm3 with Kc in mol/m3 (Kc *= 1e6^dnu), falloff rates x [M]
+# in mol/cm3, Troe c = -4.0 - 0.67 log10 Fcent. It is the default everywhere.
 CONV_KC_UNIT_SLIP = 1
 CONV_FALLOFF_XM = 2
 CONV_DOC_COVG = 4
+CONV_TROE_C4 = 16
+CONV_REFERENCE = CONV_KC_UNIT_SLIP | CONV_FALLOFF_XM | CONV_TROE_C4
 
 
 class MechanismError(ValueError):
@@ -332,7 +338,7 @@ def get_path(lib_dir: str, name: str) -> str:
 class Mechanism:
     """Gas and/or surface mechanism compiled into the flat SI tables of br_mech_desc."""
 
-    def __init__(self, gas_species, thermo, gas_rxns=(), surf=None, conv=0, p_std=1e5):
+    def __init__(self, gas_species, thermo, gas_rxns=(), surf=None, conv=CONV_REFERENCE, p_std=1e5):
         self.gas_species = [g.upper() for g in gas_species]
         self.ng = len(self.gas_species)
         self.thermo = thermo
@@ -364,7 +370,8 @@ class Mechanism:
         self._flatten()
 
     @classmethod
-    def from_files(cls, lib_dir, gas_mech=None, surface_mech=None, gasphase=None, conv=0, p_std=1e5):
+    def from_files(cls, lib_dir, gas_mech=None, surface_mech=None, gasphase=None, conv=CONV_REFERENCE,
+                   p_std=1e5):
         thermo = read_therm(get_path(lib_dir, "therm.dat"))
         rxns = []
         if gas_mech:

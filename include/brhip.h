@@ -34,15 +34,21 @@ extern "C" {
 #define BR_ERR_MAXSTEPS  -1   /* CVODE CV_TOO_MUCH_WORK  */
 #define BR_ERR_ERRTEST   -3   /* CVODE CV_ERR_FAILURE     */
 #define BR_ERR_CONV      -4   /* CVODE CV_CONV_FAILURE    */
-#define BR_ERR_UNSTABLE  -7   /* runaway state (SciML ReturnCode.Unstable analogue; br_opts.unstable_factor) */
+#define BR_ERR_UNSTABLE  -7   /* NaN state (SciML ReturnCode.Unstable), or the opt-in runaway test of
+                                 br_opts.unstable_factor */
 #define BR_ERR_INPUT    -10
 #define BR_ERR_HIP      -20
 #define BR_ERR_UNSUPPORTED -30
 
-/* convention switches (bitmask); see DESIGN.md "Parity status" */
-#define BR_CONV_KC_UNIT_SLIP  1   /* Kc *= (1e6)^dnu for non-falloff reversible reactions */
-#define BR_CONV_FALLOFF_XM    2   /* falloff net rate *= [M]                              */
-#define BR_CONV_DOC_COVG      4   /* no Asv on dtheta/dt (docs sample, predates :345)     */
+/* convention switches (bitmask); 0 = textbook CHEMKIN-II in SI units. BR_CONV_REFERENCE is what
+ * the reference's GasphaseReactions does (identified from its golden output):
+ * rates in mol/cm3 with Kc = Kp (p0/RT)^dnu in mol/m3, falloff rates also x [M] (mol/cm3), Troe
+ * c = -4.0 - 0.67 log10 Fcent. */
+#define BR_CONV_KC_UNIT_SLIP  1   /* Kc *= (1e6)^dnu for every reversible reaction          */
+#define BR_CONV_FALLOFF_XM    2   /* falloff net rate *= [M] in mol/cm3 (1e-6 [M]_SI)       */
+#define BR_CONV_DOC_COVG      4   /* no Asv on dtheta/dt (docs sample, predates :345)      */
+#define BR_CONV_TROE_C4      16   /* Troe c = -4.0 - 0.67 log10 Fcent                       */
+#define BR_CONV_REFERENCE    (BR_CONV_KC_UNIT_SLIP | BR_CONV_FALLOFF_XM | BR_CONV_TROE_C4)
 
 typedef struct br_mech br_mech;
 
@@ -84,11 +90,22 @@ typedef struct br_opts {
     int device;               /* HIP device ordinal for br_mech_create             */
     double hmax;              /* 0 = unbounded                                     */
     int trace_cap;            /* br_integrate_traced: max accepted steps recorded  */
-    double unstable_factor;   /* stop a reactor with BR_ERR_UNSTABLE once max_k |u_k| exceeds
-                                 factor * sum_k |u0_k| (0 = default 10, < 0 = never)     */
+    double unstable_factor;   /* > 0: also stop a reactor with BR_ERR_UNSTABLE once max_k |u_k|
+                                 exceeds factor * sum_k |u0_k| (not a reference behaviour;
+                                 default 0 = only a NaN state stops it, as SciML's check) */
+    int ignition_species;     /* 1-based gas species index k+1 whose max dX_k/dt over the accepted
+                                 steps marks ignition (br_stats.t_ign; OH for the reference's
+                                 ignition marker); 0 = not tracked                          */
+    int nout;                 /* dense output: number of output times (0 = none)            */
+    const double* tout;       /* [nout] ascending output times, shared by all reactors; the
+                                 state there is CVODE's CV_NORMAL output (CVodeGetDky(t, 0) on
+                                 the step that passes t), the step sequence is unchanged     */
+    double* yout;             /* [N][nout][n] states at tout (host memory for br_integrate,
+                                 device memory for br_integrate_dev); rows with tout > tf are
+                                 left untouched                                             */
 } br_opts;
 
-#define BR_NSTAT 16
+#define BR_NSTAT 20
 typedef struct br_stats {     /* per reactor; counters as CVODE's, then device cycles */
     double nsteps, nfe, nje, nsetups, nni, ncfn, netf, status;
     double cyc_total;         /* wall clock ticks (100 MHz) for the whole reactor  */
@@ -96,6 +113,10 @@ typedef struct br_stats {     /* per reactor; counters as CVODE's, then device c
     double t_end;             /* time reached                                      */
     double cyc_ctl;           /* shader clocks in the step controller (diagnostic build) */
     double cyc_clk;           /* shader clocks for the whole reactor (diagnostic build)  */
+    double t_ign;             /* ignition time: midpoint of the accepted step with the largest
+                                 dX_k/dt, k = br_opts.ignition_species (NaN if not tracked) */
+    double ign_rate;          /* that largest dX_k/dt [1/s]                                */
+    double reserved[2];
 } br_stats;
 
 int         br_version(void);
@@ -136,7 +157,9 @@ int br_integrate_traced(br_mech* m, int N, const double* T, const double* Asv, d
                         const double* tf, const br_opts* opts, br_stats* stats, double* trace);
 
 /* device-buffer entry point: all pointers are device memory on m's device; `stream` is a
- * hipStream_t (NULL = default stream). Asynchronous: returns after the launch. */
+ * hipStream_t (NULL = default stream). Asynchronous: returns after the launch. Calls on one
+ * handle share its workspaces (work counter, Jacobian / LU slots, timing events): they must be
+ * ordered on one stream (or synchronised); concurrent integrations need one handle each. */
 int br_integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv, double* du,
                      const double* dtf, const br_opts* opts, br_stats* dstats, void* stream);
 

@@ -1365,11 +1365,14 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
     if ((cv->tn + cv->h - cv->tstop) * cv->h > 0.0) cv->h = (cv->tstop - cv->tn) * (1.0 - 4.0 * cv->uround);
     cv->hscale = cv->h; cv->hprime = cv->h;
     for (int i = 0; i < n; ++i) cv->zn[1][i] *= cv->h;
-    double ufac = (o && o->unstable_factor != 0.0) ? o->unstable_factor : 10.0, uscale = 0.0;
+    double ufac = o ? o->unstable_factor : 0.0, uscale = 0.0;   /* <= 0: NaN check only */
     for (int i = 0; i < n; ++i) uscale += fabs(u[i]);
     int status = 0;
     long nstloc = 0;
     int iout = 0;
+    int ign = (o && o->ignition_species > 0 && o->ignition_species <= m->ng) ? o->ignition_species - 1 : -1;
+    double ign_x = 0.0, ign_t = 0.0, ign_rate = -INFINITY, t_ign = NAN;
+    if (ign >= 0) { double g = 0; for (int k = 0; k < m->ng; ++k) g += u[k] / m->M[k]; ign_x = (u[ign] / m->M[ign]) / g; }
     while (iout < nout && tout[iout] <= 0.0) { memcpy(yout + (size_t)iout * n, u, sizeof(double) * (size_t)n); ++iout; }
     for (;;) {
         if (cv->nst > 0) set_ewt(cv, cv->zn[0]);
@@ -1377,14 +1380,21 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
         int kf = cv_step(cv);
         if (kf) { status = kf; break; }
         nstloc++;
-        if (ufac > 0.0) {   /* runaway: a component far outside the physical range */
+        {   /* SciML unstable_check (NaN), or the opt-in runaway test */
             double mx = 0.0;
-            for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(cv->zn[0][i]));
-            if (!(mx <= ufac * uscale)) { status = -7; break; }
+            for (int i = 0; i < n; ++i) { double a = fabs(cv->zn[0][i]); mx = fmax(mx, a == a ? a : INFINITY); }
+            if (!(mx < INFINITY) || (ufac > 0.0 && mx > ufac * uscale)) { status = -7; break; }
+        }
+        if (ign >= 0) {   /* ignition marker on the accepted states */
+            double g = 0; for (int k = 0; k < m->ng; ++k) g += cv->zn[0][k] / m->M[k];
+            double x = (cv->zn[0][ign] / m->M[ign]) / g, r = (x - ign_x) / (cv->tn - ign_t);
+            if (r > ign_rate) { ign_rate = r; t_ign = 0.5 * (ign_t + cv->tn); }
+            ign_x = x; ign_t = cv->tn;
         }
         while (iout < nout && tout[iout] <= cv->tn) { get_dky(cv, tout[iout], yout + (size_t)iout * n); ++iout; }
         double troundoff = FUZZ_FACTOR * cv->uround * (fabs(cv->tn) + fabs(cv->h));
         if (fabs(cv->tn - cv->tstop) <= troundoff) {
+            while (iout < nout && tout[iout] <= cv->tstop) { get_dky(cv, tout[iout], yout + (size_t)iout * n); ++iout; }
             get_dky(cv, cv->tstop, u);
             if (cb) cb(user, cv->tstop, u, cv->p_last, cv->x_last, cv->th_last);
             break;
@@ -1400,6 +1410,7 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
         st->nsteps = cv->nst; st->nfe = cv->nfe; st->nje = cv->nje; st->nsetups = cv->nsetups;
         st->nni = cv->nni; st->ncfn = cv->ncfn; st->netf = cv->netf; st->nfeDQ = cv->nfeDQ;
         st->status = status; st->qlast = cv->q; st->hlast = cv->h; st->tcur = cv->tn;
+        st->t_ign = ign >= 0 ? t_ign : NAN; st->ign_rate = ign >= 0 ? ign_rate : NAN;
     }
     free(cv->piv); free(mem); tcache_free(&tc);
     return status;

@@ -51,8 +51,9 @@ typedef struct {
     int    analytic_jac;   /* 0 = CVODE DQ Jacobian (reference), 1 = analytic */
     int    max_steps;      /* Sundials.jl maxiters default 1e5 */
     double hmax;           /* 0 = inf */
-    double unstable_factor;/* abort (status -7) once max|u_k| > factor * sum|u0|; 0 = 10, <0 = off
-                              (DiffEq's unstable_check, see DESIGN.md "Failure detection") */
+    double unstable_factor;/* > 0: abort (status -7) once max|u_k| > factor * sum|u0| (opt-in, not a
+                              reference behaviour); always: a NaN state -> -7 (SciML unstable_check) */
+    int    ignition_species;/* 1-based gas species index whose max dX/dt marks ignition; 0 = off */
 } orc_opts;
 
 typedef struct {
@@ -61,6 +62,7 @@ typedef struct {
                               -7 unstable (runaway state) */
     int  qlast;
     double hlast, tcur;
+    double t_ign, ign_rate;/* midpoint of the accepted step with the largest dX_ign/dt, and that rate */
 } orc_stats;
 
 /* per-accepted-step callback: t, u (solver state), and the "last RHS" state

@@ -22,13 +22,15 @@ CONV_REFERENCE = CONV_KC_UNIT_SLIP | CONV_FALLOFF_XM | CONV_TROE_C4   # Gasphase
 
 class Opts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("analytic_jac", C.c_int),
-                ("max_steps", C.c_int), ("hmax", C.c_double), ("unstable_factor", C.c_double)]
+                ("max_steps", C.c_int), ("hmax", C.c_double), ("unstable_factor", C.c_double),
+                ("ignition_species", C.c_int)]
 
 
 class Stats(C.Structure):
     _fields_ = [("nsteps", C.c_long), ("nfe", C.c_long), ("nje", C.c_long), ("nsetups", C.c_long),
                 ("nni", C.c_long), ("ncfn", C.c_long), ("netf", C.c_long), ("nfeDQ", C.c_long),
-                ("status", C.c_int), ("qlast", C.c_int), ("hlast", C.c_double), ("tcur", C.c_double)]
+                ("status", C.c_int), ("qlast", C.c_int), ("hlast", C.c_double), ("tcur", C.c_double),
+                ("t_ign", C.c_double), ("ign_rate", C.c_double)]
 
     def asdict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -97,7 +99,8 @@ def _enc(s):
 class Mech:
     """One compiled mechanism (gas and/or surface) for the oracle."""
 
-    def __init__(self, gas_mech=None, therm=None, surf_mech=None, gas_species=None, conv=0, p_std=1e5):
+    def __init__(self, gas_mech=None, therm=None, surf_mech=None, gas_species=None, conv=CONV_REFERENCE,
+                 p_std=1e5):
         L = lib()
         gs = " ".join(gas_species) if gas_species else None
         self.h = L.orc_load(_enc(gas_mech), _enc(therm), _enc(surf_mech), _enc(gs), conv, p_std)
@@ -110,6 +113,7 @@ class Mech:
         self.M = np.array([L.orc_molwt(self.h, k) for k in range(self.ng)])
         self.site_density = L.orc_site_density(self.h)
         self.theta0 = np.zeros(self.ns)
+        self.ign1 = self.names.index("OH") + 1 if "OH" in self.names[:self.ng] else 0   # ignition marker
         if self.ns:
             L.orc_initial_coverage(self.h, _p(self.theta0))
 
@@ -164,7 +168,7 @@ class Mech:
     def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, analytic_jac=False, max_steps=100000,
                   record=False):
         u = np.array(u0, dtype=np.float64)
-        o = Opts(rtol, atol, int(analytic_jac), max_steps, 0.0)
+        o = Opts(rtol, atol, int(analytic_jac), max_steps, 0.0, 0.0, self.ign1)
         st = Stats()
         rows = []
         ng, ns = self.ng, self.ns
@@ -183,7 +187,7 @@ class Mech:
         u = np.array(u0, dtype=np.float64)
         tout = np.ascontiguousarray(tout, dtype=np.float64)
         Y = np.zeros((len(tout), self.n))
-        o = Opts(rtol, atol, int(analytic_jac), max_steps, 0.0)
+        o = Opts(rtol, atol, int(analytic_jac), max_steps, 0.0, 0.0, self.ign1)
         st = Stats()
         lib().orc_integrate_out(self.h, T, Asv, _p(u), tf, C.byref(o), C.byref(st), len(tout), _p(tout), _p(Y))
         return u, st.asdict(), Y
@@ -194,7 +198,7 @@ class Mech:
         T = np.ascontiguousarray(T, dtype=np.float64)
         Asv = np.ascontiguousarray(Asv, dtype=np.float64)
         tf = np.ascontiguousarray(np.broadcast_to(tf, (N,)), dtype=np.float64)
-        o = Opts(rtol, atol, int(analytic_jac), 100000, 0.0)
+        o = Opts(rtol, atol, int(analytic_jac), 100000, 0.0, 0.0, self.ign1)
         st = (Stats * N)()
         bad = lib().orc_integrate_batch(self.h, N, _p(T), _p(Asv), _p(U), _p(tf), C.byref(o), st, nthreads)
         return U, [s.asdict() for s in st], bad

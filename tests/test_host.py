@@ -82,3 +82,90 @@ def test_state_to_molefrac_roundtrip(pkg):
     x = m.mole_fractions({"H2": 0.25, "O2": 0.25, "N2": 0.5})
     u = m.initial_state(1173.0, 1e5, x)
     np.testing.assert_allclose(m.state_to_molefrac(u), x, rtol=1e-15, atol=1e-16)
+
+
+def test_csv_writer_is_julia_string_format(pkg):
+    """save_data writes CSV through Julia's string(::Float64) (src/BatchReactor.jl:395-399,
+    RxnHelperUtils.write_csv): every number token of the reference's own gas+surf CSVs (committed
+    fixture rows, tokens verbatim) is reproduced character for character (e-5, not e-05; 1.0e-5;
+    100000.0; 0.0001)."""
+    import csv
+    n = 0
+    for name in ("gas_and_surf_golden.csv", "gas_and_surf_covg_golden.csv"):
+        for r in list(csv.reader(open(os.path.join(GOLDEN, name))))[1:]:
+            for tok in r[1:]:
+                assert pkg.julia_string(float(tok)) == tok, tok
+                n += 1
+    assert n > 20000
+    for v, s in ((1e6, "1.0e6"), (123456.7, "123456.7"), (1e-5, "1.0e-5"), (-2.5e-7, "-2.5e-7"), (0.0, "0.0"),
+                 (1173.0, "1173.0"), (10.0, "10.0")):
+        assert pkg.julia_string(v) == s
+
+
+def _udf_dir(tmp_path):
+    import shutil
+    d = tmp_path / "batch_udf"
+    d.mkdir()
+    shutil.copy(os.path.join(GOLDEN, "batch_udf", "batch.xml"), d / "batch.xml")
+    return d
+
+
+def test_udf_zero_source_success(pkg, tmp_path):
+    """Reference testset "Testing user defined chemistry" (test/runtests.jl:70-77): a udf that sets
+    state.source to zero returns Success; the gas profile rows keep the inlet state."""
+    d = _udf_dir(tmp_path)
+
+    def udf(state):
+        state.source[:] = 0.0
+    assert pkg.batch_reactor(str(d / "batch.xml"), LIB, udf) == "Success"
+    rows = open(d / "gas_profile.csv").read().splitlines()
+    assert rows[0] == "t,T,p,rho,CH4,H2O,H2,CO,CO2,O2,N2"
+    last = rows[-1].split(",")
+    assert float(last[0]) == 10.0 and last[4:] == ["0.25", "0.25", "0.0", "0.0", "0.0", "0.0", "0.5"]
+    assert open(d / "surface_covg.csv").read() == ""          # opened, never written (:171-173)
+
+
+def test_udf_source_integrates(pkg, tmp_path):
+    """A constant udf source S_k [mol/m3/s] gives rho_k(t) = rho_k(0) + S_k M_k t exactly
+    (du = source .* molwt, src/BatchReactor.jl:371-372); the state handed to the udf keeps the inlet
+    T, p and mole fractions (residual! never updates u_state, :358-360)."""
+    d = _udf_dir(tmp_path)
+    seen = []
+
+    def udf(state):
+        seen.append((state.T, state.p, state.mole_frac.copy()))
+        state.source[:] = 0.0
+        state.source[state.species.index("H2")] = 1e-3
+        state.source[state.species.index("CH4")] = -1e-4
+    assert pkg.batch_reactor(str(d / "batch.xml"), LIB, udf) == "Success"
+    rows = [r.split(",") for r in open(d / "gas_profile.csv").read().splitlines()[1:]]
+    m = pkg.Mechanism.from_files(LIB, gasphase="CH4 H2O H2 CO CO2 O2 N2".split())
+    rho0 = m.initial_state(1073.15, 1e5, m.mole_fractions({"CH4": 0.25, "H2O": 0.25, "N2": 0.5})).sum()
+    dM = 1e-3 * m.molwt[2] - 1e-4 * m.molwt[0]
+    for r in rows:
+        assert abs(float(r[3]) - (rho0 + dM * float(r[0]))) <= 1e-9 * rho0
+    assert all(s[0] == 1073.15 and s[1] == 1e5 for s in seen)
+
+
+def test_sens_returns_params_prob_tspan(pkg, tmp_path):
+    """sens=true returns (params, prob, t_span) (src/BatchReactor.jl:205-207): params carries the
+    reference's fields, prob.f is residual!(du, u, p, t)."""
+    d = _udf_dir(tmp_path)
+
+    def udf(state):
+        state.source[:] = 2.0
+    params, prob, t_span = pkg.batch_reactor(str(d / "batch.xml"), LIB, udf, sens=True)
+    assert t_span == (0.0, 10.0) and prob.tspan == t_span
+    assert set(params) == {"s_state", "g_state", "u_state", "thermo", "smd", "gmd", "cp", "chem"}
+    assert params["cp"].Asv == 10.0 and params["cp"].T == 1073.15 and params["chem"].userchem
+    du = np.zeros_like(prob.u0)
+    prob.f(du, prob.u0, prob.p, 0.0)
+    np.testing.assert_allclose(du, 2.0 * params["thermo"].molwt)
+
+
+def test_reference_conventions_are_default(pkg, orc):
+    """The reference's gas-kinetics conventions (CONV_REFERENCE) are the
+    default of the product compiler and of the oracle; textbook CHEMKIN stays available (conv=0)."""
+    m = pkg.Mechanism.from_files(LIB, gas_mech="grimech.dat")
+    assert m.conv == pkg.CONV_REFERENCE == orc.CONV_REFERENCE == 19
+    assert pkg.Mechanism.from_files(LIB, gas_mech="h2o2.dat", conv=0).conv == 0

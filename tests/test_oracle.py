@@ -25,7 +25,8 @@ def _golden(name):
 
 @pytest.fixture(scope="module")
 def gs_mech(orc):
-    return orc.Mech(os.path.join(LIB, "grimech.dat"), TH, os.path.join(LIB, "ch4ni.xml"))
+    """textbook CHEMKIN-II gas kinetics (conv 0)"""
+    return orc.Mech(os.path.join(LIB, "grimech.dat"), TH, os.path.join(LIB, "ch4ni.xml"), conv=0)
 
 
 @pytest.fixture(scope="module")
