@@ -28,7 +28,8 @@ class MechDesc(C.Structure):
 class Opts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("max_steps", C.c_int), ("device", C.c_int),
                 ("hmax", C.c_double), ("trace_cap", C.c_int), ("unstable_factor", C.c_double),
-                ("ignition_species", C.c_int), ("nout", C.c_int), ("tout", dp), ("yout", dp)]
+                ("ignition_species", C.c_int), ("nout", C.c_int), ("tout", dp), ("yout", dp),
+                ("dq_jacobian", C.c_int)]
 
 
 NSTAT = 20

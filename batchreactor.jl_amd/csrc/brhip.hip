@@ -45,6 +45,7 @@ struct KOpts {
     int nout;                 // dense output: tout[nout] (device), yout[N][nout][n] (device)
     const double* tout;
     double* yout;
+    int dq_jac;               // k_lane: CVODE's DQ Jacobian (br_opts.dq_jacobian) instead of the analytic one
     int defer_steps;          // k_lane: hand a reactor still running after this many steps to the
                               // wavefront engine (restart from u0); >= max_steps disables
     const int* rid_list;      // k_integrate: integrate reactors rid_list[0 .. min(*rid_count, N)) only
@@ -73,7 +74,7 @@ struct Ctl {
     int ncf, nef, nstloc, status, m_it, convfail, count1, phase;
     int callSetup, jbad, jcur_nls, hnewOK, newj;
     // ignition marker (max dX_ign/dt over accepted steps) and dense-output cursor
-    double ign_x, ign_t, ign_rate, t_ign;
+    double ign_x, ign_t, ign_rate, t_ign, ign_dt;
     int iout;
     // per-launch constants (here rather than in registers: they are read once per step)
     double a_rtol, a_atol, a_hmax_inv, a_ufac;
@@ -207,7 +208,7 @@ __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int la
     const double x = uni(mole_frac_of<CPL>(v, lane, a.ign));
     const double t0 = ud(C->ign_t);
     const double r = (x - ud(C->ign_x)) / (tn - t0);
-    if (r > ud(C->ign_rate)) { C->ign_rate = r; C->t_ign = 0.5 * (t0 + tn); }
+    if (r > ud(C->ign_rate)) { C->ign_rate = r; C->t_ign = 0.5 * (t0 + tn); C->ign_dt = tn - t0; }
     C->ign_x = x; C->ign_t = tn;
 }
 // dense output (CVode CV_NORMAL): every tout in (t_{n-1}, t_n] from the Nordsieck array of the step
@@ -924,7 +925,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     C->nstlj = 0; C->ncf = 0; C->nef = 0; C->nstloc = 0; C->status = 0; C->m_it = 0; C->convfail = 0;
     C->count1 = 0; C->phase = PH_F0; C->callSetup = 0; C->jbad = 0; C->jcur_nls = 0; C->hnewOK = 0; C->newj = 0;
     C->p_last = 0.0;
-    C->iout = 0; C->ign_t = 0.0; C->ign_rate = -INFINITY; C->t_ign = NAN; C->ign_x = 0.0;
+    C->iout = 0; C->ign_t = 0.0; C->ign_rate = -INFINITY; C->t_ign = NAN; C->ign_x = 0.0; C->ign_dt = NAN;
     if (o.ign >= 0) C->ign_x = uni(mole_frac_of<CPL>(u0, lane, o.ign));
     if (o.nout) {                                           // outputs at t <= 0: the initial state
         int io = 0;
@@ -1016,7 +1017,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
 #endif
         st[13] = ud(C->tn);
         st[16] = o.ign >= 0 ? ud(C->t_ign) : NAN; st[17] = o.ign >= 0 ? ud(C->ign_rate) : NAN;
-        st[18] = st[19] = 0.0;
+        st[18] = o.ign >= 0 ? ud(C->ign_dt) : NAN; st[19] = 0.0;
     }
     }   // next reactor
 }
@@ -1584,6 +1585,7 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.nout = (opts && opts->nout > 0 && opts->tout && opts->yout) ? opts->nout : 0;
     o.tout = o.nout ? opts->tout : nullptr;
     o.yout = o.nout ? opts->yout : nullptr;
+    o.dq_jac = (opts && opts->dq_jacobian) ? 1 : 0;
     o.defer_steps = o.max_steps;
     o.rid_list = nullptr;
     o.rid_count = nullptr;

@@ -126,7 +126,7 @@ struct LCV {
     int q, qprime, L, qwait, nst, nfe, nsetups, nje, nni, ncfn, netf, nstlp, nstlj;
     int ncf, nef, nstloc, status, m_it, convfail, count1, phase, callSetup, jbad, jcur_nls, hnewOK, jcol;
     int pend, pflag;   // deferred step/attempt start (one call site in the kernel): PEND_*, nflag
-    double ign_x, ign_t, ign_rate, t_ign;   // ignition marker (max dX_ign/dt over accepted steps)
+    double ign_x, ign_t, ign_rate, t_ign, ign_dt;   // ignition marker (max dX_ign/dt over accepted steps)
     int iout, rid;                          // dense-output cursor, reactor index
 };
 
@@ -450,6 +450,10 @@ __device__ __forceinline__ int l_post_rhs(LCV& c, ZH<NM>& z, double (&acor)[NM],
             c.nsetups += 1;
             c.jcur_nls = newj;
             c.gamrat = 1.0; c.gammap = c.gamma; c.crate = 1.0; c.nstlp = c.nst;
+            if (newj && !o.dq_jac) {            // analytic Jacobian at y (the RHS point just evaluated)
+                lane_jac<NM>(LL, Lp, G, n);
+                return A_SETUP;
+            }
             if (newj) {                         // DQ Jacobian at (y, f): n more RHS iterations
                 const double fnorm = lwrms<NM>(f, ewt, n);
                 c.minInc = (fnorm != 0.0) ? (MIN_INC_MULT * fabs(c.h) * UROUND * n * fnorm) : 1.0;
@@ -693,7 +697,7 @@ __device__ __forceinline__ int l_post_solve(LCV& c, ZH<NM>& z, double (&acor)[NM
     if (o.ign >= 0) {                            // ignition marker (midpoint of the steepest step)
         const double x = l_mole_frac<NM>(z.z0, n, o.ign);
         const double r = (x - c.ign_x) / (c.tn - c.ign_t);
-        if (r > c.ign_rate) { c.ign_rate = r; c.t_ign = 0.5 * (c.ign_t + c.tn); }
+        if (r > c.ign_rate) { c.ign_rate = r; c.t_ign = 0.5 * (c.ign_t + c.tn); c.ign_dt = c.tn - c.ign_t; }
         c.ign_x = x; c.ign_t = c.tn;
     }
     const double tlim = fabs(c.tn - c.tstop) <= FUZZ * UROUND * (fabs(c.tn) + fabs(h)) ? c.tstop : c.tn;
@@ -985,6 +989,88 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
     for (int k = 0; k < NM; ++k) f[k] = (k < n) ? Lp[(LL.acc + k) * 64] * mw[k] : 0.0;
 }
 
+// analytic Jacobian d(du)/du of the lane's reactor (gas only, du_k = M_k sum_r nu_kr q_r,
+// c_j = u_j / M_j), at the state of the RHS just evaluated (its concentrations and third-body sums
+// are still in the lane's LDS rows), column-major into the lane's saved-J rows: element (i, j) at
+// row j * NM + i. Same derivative terms as the wavefront engine and the oracle (jac_tc):
+// mass-action partial products, third-body / falloff d[M] columns.
+template <int NM>
+__device__ __noinline__ void lane_jac(const LaneLay& LL, const double* Lp, const GRows& G, int n) {
+    const CF64* mw = (const CF64*)MF(img);
+    const bool xm = (MF(conv) & 2) != 0;
+    const int nrg = MF(nrg);
+    const CU32* rx = (const CU32*)((const char*)MF(img) + Lay<1>::IMG_RX);
+    const CU32* tbs = (const CU32*)((const char*)MF(img) + MF(tbs_off));
+    const char* tbe = (const char*)MF(img) + MF(tbe_off);
+#pragma unroll
+    for (int j = 0; j < NM; ++j)
+#pragma unroll
+        for (int i = 0; i < NM; ++i) G.st(j * NM + i, 0.0);
+    for (int r = 0; r < nrg; ++r) {
+        const CU32* rec = rx + RX_WORDS * r;
+        const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], s0 = rec[4], s1 = rec[5], s2 = rec[6];
+        const double kf = G.ld(LL.g_rxd + 2 * r), kr = G.ld(LL.g_rxd + 2 * r + 1);
+        double cf[4], cb[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            cf[e] = Lp[(LL.conc + lane_sp(w0, e, n)) * 64];
+            cb[e] = Lp[(LL.conc + lane_sp(w1, e, n)) * 64];
+        }
+        const double D = kf * (cf[0] * cf[1] * cf[2] * cf[3]) - kr * (cb[0] * cb[1] * cb[2] * cb[3]);
+        double pre = 1.0, coefM = 0.0;
+        const int tbk = gi_tb(info);
+        if (tbk) {
+            const double Mc = Lp[(LL.mc + gi_tbidx(info)) * 64];
+            if (tbk == 1) { pre = Mc; coefM = 1.0; }
+            else {
+                const int fi = gi_foidx(info);
+                double fo[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) fo[c] = G.ld(LL.g_fod + 4 * fi + c);
+                double fac, dfac;
+                falloff<true>(fo, gi_troe(info) != 0, kf, Mc, fac, dfac);
+                const double xs = xm ? Mc * 1e-6 : 1.0;                   // [M] in mol/cm3 (reference)
+                pre = fac * xs;
+                coefM = dfac * xs + (xm ? fac * 1e-6 : 0.0);
+            }
+        }
+        double dq[NM];                                                 // d q_r / d c_j
+#pragma unroll
+        for (int j = 0; j < NM; ++j) dq[j] = tbk ? D * coefM : 0.0;
+        if (tbk) {                                                     // non-unit efficiencies
+            const uint32_t w = tbs[gi_tbidx(info)];
+            const int b = w & 0xFFFFF, e = b + (int)(w >> 20);
+            for (int t = b; t < e; ++t) {
+                const int k = *(const CU32*)(tbe + 16 * t) & 0xFFFF;
+                const double em1 = *(const CF64*)(tbe + 16 * t + 8);
+#pragma unroll
+                for (int j = 0; j < NM; ++j) dq[j] += (j == k) ? D * coefM * em1 : 0.0;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int kfs = (int)((w0 >> (8 * e)) & 255), kbs = (int)((w1 >> (8 * e)) & 255);
+            double pf = kf * pre, pb = -kr * pre;
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) if (e2 != e) { pf *= cf[e2]; pb *= cb[e2]; }
+#pragma unroll
+            for (int j = 0; j < NM; ++j) {
+                dq[j] += (j == kfs) ? pf : 0.0;                         // pad slots (SP_ONE) match no j
+                dq[j] += (j == kbs) ? pb : 0.0;
+            }
+        }
+        const int cnt = (s1 >> 16) & 255;
+        for (int e = 0; e < cnt; ++e) {                                // rows of the touched species
+            const int k = e < 4 ? (int)((s0 >> (8 * e)) & 255) : (int)((s1 >> (8 * (e - 4))) & 255);
+            const int nu = ((int)(s2 << (28 - 4 * e))) >> 28;
+            const double sk = (double)nu * mw[k];
+#pragma unroll
+            for (int j = 0; j < NM; ++j)
+                if (j < n) G.st(j * NM + k, G.ld(j * NM + k) + sk * dq[j] / mw[j]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // the lane integrator kernel (persistent grid; 64-thread workgroups, one wave each)
 // ------------------------------------------------------------------------------------
@@ -1053,7 +1139,7 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
                 c.nstlp = 0; c.nstlj = 0; c.ncf = 0; c.nef = 0; c.nstloc = 0; c.status = 0; c.m_it = 0;
                 c.convfail = 0; c.count1 = 0; c.phase = PH_F0; c.callSetup = 0; c.jbad = 0; c.jcur_nls = 0;
                 c.hnewOK = 0; c.jcol = 0; c.pend = PEND_NONE; c.pflag = 0;
-                c.rid = rid; c.iout = 0; c.ign_t = 0.0; c.ign_rate = -INFINITY; c.t_ign = NAN;
+                c.rid = rid; c.iout = 0; c.ign_t = 0.0; c.ign_rate = -INFINITY; c.t_ign = NAN; c.ign_dt = NAN;
                 c.ign_x = o.ign >= 0 ? l_mole_frac<NM>(y, n, o.ign) : 0.0;
                 while (c.iout < o.nout && !(o.tout[c.iout] > 0.0)) {   // outputs at t <= 0: u0
                     double* row = o.yout + ((size_t)rid * o.nout + c.iout) * n;
@@ -1143,7 +1229,7 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
 #endif
                 st[13] = c.tn;
                 st[16] = o.ign >= 0 ? c.t_ign : NAN; st[17] = o.ign >= 0 ? c.ign_rate : NAN;
-                st[18] = st[19] = 0.0;
+                st[18] = o.ign >= 0 ? c.ign_dt : NAN; st[19] = 0.0;
             }
             has = false;
         }

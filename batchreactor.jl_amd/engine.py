@@ -18,8 +18,8 @@ from . import _lib
 from .mechanism import Mechanism
 
 STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status", "cyc_total", "cyc_rhs",
-               "cyc_jac", "cyc_lu", "cyc_sol", "t_end", "cyc_ctl", "cyc_clk", "t_ign", "ign_rate", "reserved0",
-               "reserved1")
+               "cyc_jac", "cyc_lu", "cyc_sol", "t_end", "cyc_ctl", "cyc_clk", "t_ign", "ign_rate", "ign_dt",
+               "reserved")
 IGNITION_MARKER = "OH"   # the reference golden's ignition marker: max dX_OH/dt
 
 
@@ -118,25 +118,26 @@ class Engine:
         _lib.check(_lib.lib().br_jacobian(self.h, N, _lib.dptr(T), _lib.dptr(A), _lib.dptr(u), _lib.dptr(J)))
         return J
 
-    def _opts(self, rtol, atol, max_steps, trace_cap=0, unstable_factor=0.0, tout=None, yout=None):
+    def _opts(self, rtol, atol, max_steps, trace_cap=0, unstable_factor=0.0, tout=None, yout=None, dq_jacobian=False):
         nout = 0 if tout is None else len(tout)
         return _lib.Opts(rtol, atol, max_steps, self.device, 0.0, trace_cap, unstable_factor, self.ign1, nout,
-                         _lib.dptr(tout) if nout else None, _lib.dptr(yout) if nout else None)
+                         _lib.dptr(tout) if nout else None, _lib.dptr(yout) if nout else None, int(dq_jacobian))
 
     def integrate(self, T, Asv, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000, trace_cap=0, tout=None,
-                  unstable_factor=0.0):
+                  unstable_factor=0.0, dq_jacobian=False):
         """Integrate N reactors 0 -> tf. With trace_cap > 0 also returns the per-step rows
         trace[N, trace_cap+1, 2n+4] = (t, h, q, p_last, u[n], y_last[n]): u the accepted state, y_last
         and p_last the state and pressure of the step's last RHS evaluation (save_data semantics).
         With tout (ascending output times) the stats dict also carries "yout" [N, nout, n], the
-        states at those times (CVODE CV_NORMAL output, the step sequence is unchanged)."""
+        states at those times (CVODE CV_NORMAL output, the step sequence is unchanged).
+        dq_jacobian: CVODE's difference-quotient Jacobian (the reference's setting) in the lane engine."""
         u = np.array(np.atleast_2d(u0), dtype=np.float64, order="C")
         N = u.shape[0]
         T, A, tf = self._arr(T, N), self._arr(Asv, N), self._arr(tf, N)
         st = np.zeros((N, _lib.NSTAT))
         to = None if tout is None else np.ascontiguousarray(tout, dtype=np.float64)
         yo = None if tout is None else np.zeros((N, len(to), self.n))
-        o = self._opts(rtol, atol, max_steps, trace_cap, unstable_factor, to, yo)
+        o = self._opts(rtol, atol, max_steps, trace_cap, unstable_factor, to, yo, dq_jacobian)
         L = _lib.lib()
         if trace_cap > 0:
             tr = np.zeros((N, trace_cap + 1, 2 * self.n + 4))

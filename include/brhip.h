@@ -103,6 +103,9 @@ typedef struct br_opts {
     double* yout;             /* [N][nout][n] states at tout (host memory for br_integrate,
                                  device memory for br_integrate_dev); rows with tout > tf are
                                  left untouched                                             */
+    int dq_jacobian;          /* 1: CVODE's dense difference-quotient Jacobian (the reference's
+                                 CVODE_BDF() setting) in the one-reactor-per-lane engine;
+                                 0 (default): the analytic Jacobian, as the wavefront engine */
 } br_opts;
 
 #define BR_NSTAT 20
@@ -116,7 +119,8 @@ typedef struct br_stats {     /* per reactor; counters as CVODE's, then device c
     double t_ign;             /* ignition time: midpoint of the accepted step with the largest
                                  dX_k/dt, k = br_opts.ignition_species (NaN if not tracked) */
     double ign_rate;          /* that largest dX_k/dt [1/s]                                */
-    double reserved[2];
+    double ign_dt;            /* width of that step (the resolution of t_ign) [s]            */
+    double reserved;
 } br_stats;
 
 int         br_version(void);

@@ -1371,7 +1371,7 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
     long nstloc = 0;
     int iout = 0;
     int ign = (o && o->ignition_species > 0 && o->ignition_species <= m->ng) ? o->ignition_species - 1 : -1;
-    double ign_x = 0.0, ign_t = 0.0, ign_rate = -INFINITY, t_ign = NAN;
+    double ign_x = 0.0, ign_t = 0.0, ign_rate = -INFINITY, t_ign = NAN, ign_dt = NAN;
     if (ign >= 0) { double g = 0; for (int k = 0; k < m->ng; ++k) g += u[k] / m->M[k]; ign_x = (u[ign] / m->M[ign]) / g; }
     while (iout < nout && tout[iout] <= 0.0) { memcpy(yout + (size_t)iout * n, u, sizeof(double) * (size_t)n); ++iout; }
     for (;;) {
@@ -1388,7 +1388,7 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
         if (ign >= 0) {   /* ignition marker on the accepted states */
             double g = 0; for (int k = 0; k < m->ng; ++k) g += cv->zn[0][k] / m->M[k];
             double x = (cv->zn[0][ign] / m->M[ign]) / g, r = (x - ign_x) / (cv->tn - ign_t);
-            if (r > ign_rate) { ign_rate = r; t_ign = 0.5 * (ign_t + cv->tn); }
+            if (r > ign_rate) { ign_rate = r; t_ign = 0.5 * (ign_t + cv->tn); ign_dt = cv->tn - ign_t; }
             ign_x = x; ign_t = cv->tn;
         }
         while (iout < nout && tout[iout] <= cv->tn) { get_dky(cv, tout[iout], yout + (size_t)iout * n); ++iout; }
@@ -1411,6 +1411,7 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
         st->nni = cv->nni; st->ncfn = cv->ncfn; st->netf = cv->netf; st->nfeDQ = cv->nfeDQ;
         st->status = status; st->qlast = cv->q; st->hlast = cv->h; st->tcur = cv->tn;
         st->t_ign = ign >= 0 ? t_ign : NAN; st->ign_rate = ign >= 0 ? ign_rate : NAN;
+        st->ign_dt = ign >= 0 ? ign_dt : NAN;
     }
     free(cv->piv); free(mem); tcache_free(&tc);
     return status;

@@ -63,6 +63,7 @@ typedef struct {
     int  qlast;
     double hlast, tcur;
     double t_ign, ign_rate;/* midpoint of the accepted step with the largest dX_ign/dt, and that rate */
+    double ign_dt;         /* width of that step */
 } orc_stats;
 
 /* per-accepted-step callback: t, u (solver state), and the "last RHS" state

@@ -30,7 +30,7 @@ class Stats(C.Structure):
     _fields_ = [("nsteps", C.c_long), ("nfe", C.c_long), ("nje", C.c_long), ("nsetups", C.c_long),
                 ("nni", C.c_long), ("ncfn", C.c_long), ("netf", C.c_long), ("nfeDQ", C.c_long),
                 ("status", C.c_int), ("qlast", C.c_int), ("hlast", C.c_double), ("tcur", C.c_double),
-                ("t_ign", C.c_double), ("ign_rate", C.c_double)]
+                ("t_ign", C.c_double), ("ign_rate", C.c_double), ("ign_dt", C.c_double)]
 
     def asdict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
