@@ -995,7 +995,7 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
 // row j * NM + i. Same derivative terms as the wavefront engine and the oracle (jac_tc):
 // mass-action partial products, third-body / falloff d[M] columns.
 template <int NM>
-__device__ __noinline__ void lane_jac(const LaneLay& LL, const double* Lp, const GRows& G, int n) {
+__device__ __forceinline__ void lane_jac(const LaneLay& LL, const double* Lp, const GRows& G, int n) {
     const CF64* mw = (const CF64*)MF(img);
     const bool xm = (MF(conv) & 2) != 0;
     const int nrg = MF(nrg);

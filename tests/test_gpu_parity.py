@@ -184,17 +184,21 @@ def _band_errors(Yg, Yo, tign):
     return [float(e[(r >= lo) & (r < hi)].max(initial=0.0)) for lo, hi, _ in _BANDS]
 
 
-@pytest.mark.parametrize("case,N", [("h2o2", 256), ("gri", 64), ("surf", 64), ("gas_surf", 32)])
-def test_integrate_parity(pkg, orc, gpu, case, N):
+@pytest.mark.parametrize("case,N,dq", [("h2o2", 256, False), ("gri", 64, False), ("surf", 64, False),
+                                      ("gas_surf", 32, False), ("h2o2", 256, True)],
+                         ids=["h2o2", "gri", "surf", "gas_surf", "h2o2-dq"])
+def test_integrate_parity(pkg, orc, gpu, case, N, dq):
     """Every reactor: same status (Success), the same ignition time to within the width of the
     ignition step (the marker's resolution), states at the 28 output times within the bands above,
-    the same step count to 35 % per reactor and 3 % over the slice (rounding changes step sequences)."""
+    the same step count to 35 % per reactor and 3 % over the slice (rounding changes step sequences).
+    Both engines use the analytic Jacobian by default; "h2o2-dq" runs the lane engine with CVODE's
+    DQ Jacobian (br_opts.dq_jacobian, the reference's setting) against the oracle's DQ run."""
     from batchreactor_amd import ensemble
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
-    analytic = eng.engine == "wave"           # the lane engine uses CVODE's DQ Jacobian, like the reference
+    analytic = not dq
     T, Asv, U0 = ensemble.make_inputs(pm, case, 0, N)
-    U, st = eng.integrate(T, Asv, U0, 10.0, tout=OUT_T)
+    U, st = eng.integrate(T, Asv, U0, 10.0, tout=OUT_T, dq_jacobian=dq)
     assert np.all(st["status"] == 0), np.unique(st["status"])
     worst = np.zeros(3)
     nst_o = 0
@@ -213,7 +217,7 @@ def test_integrate_parity(pkg, orc, gpu, case, N):
         assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.35 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
         nst_o += so["nsteps"]
     assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
-    print(f"\n  {case}: worst error per band (units of 1e-4|u|+1e-8): {worst}")
+    print(f"\n  {case}{' (DQ)' if dq else ''}: worst error per band (units of 1e-4|u|+1e-8): {worst}")
 
 
 def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu):
@@ -554,11 +558,11 @@ def test_dense_output_edge_cases(pkg, orc, gpu):
                 if t == tf[i]:
                     assert close_states(Y[i, j], U[i], rtol=1e-12, floor=1e-20) <= 1.0
             sel = tout <= tf[i]
-            uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], tf[i], tout[sel], analytic_jac=eng.engine == "wave")
+            uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], tf[i], tout[sel], analytic_jac=True)
             e = (np.abs(Y[i][sel] - Yo) / (1e-4 * np.abs(Yo) + 100 * ATOL)).max(axis=1)
             ti = so["t_ign"] if so["t_ign"] == so["t_ign"] else np.inf
             r = tout[sel] / ti
-            for lo, hi, bound in (_BANDS if eng.engine == "wave" else ((0.0, 0.5, DQ_PRE_IGNITION_BOUND),) + _BANDS[1:]):
+            for lo, hi, bound in _BANDS:
                 assert e[(r >= lo) & (r < hi)].max(initial=0.0) <= bound, (case, i, lo, hi)
 
 
@@ -575,14 +579,14 @@ def test_lane_engine_h2o2(pkg, orc, gpu, monkeypatch):
     N = 200
     T, Asv, U0 = _ignition_inputs(pm, "h2o2", N, 6)
     tf = np.where(np.arange(N) % 3 == 0, 1e-3, 1e-2)            # ragged end times
-    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16)
+    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16, dq_jacobian=True)
     assert np.all(st["status"] == 0)
     for i in range(N):
         uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf[i], analytic_jac=False, rtol=1e-10, atol=1e-16)
         assert so["status"] == 0
         e = close_states(U[i], uo, rtol=1e-6, floor=1e-14)
         assert e <= 1.0, (i, e)
-    U, st = eng.integrate(T, Asv, U0, 1e-2)
+    U, st = eng.integrate(T, Asv, U0, 1e-2, dq_jacobian=True)
     Ud, std_, _ = om.integrate_batch(T, Asv, U0, 1e-2, analytic_jac=False, nthreads=8)
     sd = np.array([s["status"] for s in std_])
     assert np.array_equal(st["status"] == 0, sd == 0)
