@@ -1,17 +1,23 @@
 #!/usr/bin/env python3
 """Benchmark: reactor integrations/s for the GRI-Mech 3.0 CH4 ensemble (BASELINE.json metric).
 
-One step = integrating one batch of N reactors (per GPU) from t=0 to tf=10 s with the
-CVODE-style BDF (rtol 1e-6, atol 1e-10) on MI355X. Inputs are synthetic,
-generated per rank for its own contiguous shard and resident in HBM before timing. Reactors are
-independent, so ranks share no data during integration (weak scaling: N reactors per GPU); the
-final states are all-gathered over RCCL once, after the timed region.
+One step = integrating the ensemble from t=0 to tf=10 s with the CVODE-style BDF (rtol 1e-6,
+atol 1e-10) on MI355X. Inputs are synthetic, generated per rank for its own
+contiguous shard and resident in HBM before timing. Reactors are independent, so ranks share no
+data during integration; the final states are all-gathered over RCCL once, after the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--n REACTORS_PER_GPU] [--config gri]
+Scaling (BASELINE.json: "ensemble of 1e5 reactors, sharded over 1/2/4/8 GPUs"):
+  --scaling strong (default): the config's total N (1e5 for GRI) is split into contiguous slices
+                              over the ranks;
+  --scaling weak:             every rank integrates N reactors (--n).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config gri|h2o2|surf|gas_surf]
+                  [--scaling strong|weak] [--n N] [--no-cpu] [--no-phase]
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -20,7 +26,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 dense (vector and matrix rate are equal for fp64)
+FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 dense (vector; the fp64 matrix rate is the same)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CONFIGS = {
     "gri": dict(gas="grimech.dat", surf=None, n=100000, tf=10.0,
                 name="C3 test/batch_ch4 GRI-Mech 3.0 CH4/O2/N2 ensemble (53 species, 325 reactions)"),
@@ -31,18 +38,29 @@ CONFIGS = {
 }
 
 
+def make_mech(pkg, config):
+    cfg = CONFIGS[config]
+    lib = os.path.join(ROOT, "tests", "golden", "lib")
+    return pkg.Mechanism.from_files(lib, gas_mech=cfg["gas"], surface_mech=cfg["surf"],
+                                    gasphase=None if cfg["gas"] else "CH4 H2O H2 CO CO2 O2 N2".split())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="gri", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="reactors per GPU (default: the config's N)")
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"))
+    ap.add_argument("--n", type=int, default=0, help="total reactors (strong) or reactors per GPU (weak); "
+                                                     "default: the config's N")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_gri.json"),
-                    help="PMC summary (scripts/pmc_traffic.py) giving HBM bytes per reactor for roofline.traffic")
+    ap.add_argument("--no-phase", action="store_true", help="skip the rate+Jacobian phase split (diag build)")
+    ap.add_argument("--phase-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.phase_only:
+        return phase_split(args)
 
     import torch
     import torch.distributed as dist
@@ -59,12 +77,16 @@ def main():
     pkg = _pkgload.load()
     from batchreactor_amd import ensemble, shard
     cfg = CONFIGS[args.config]
-    lib = os.path.join(ROOT, "tests", "golden", "lib")
-    mech = pkg.Mechanism.from_files(lib, gas_mech=cfg["gas"], surface_mech=cfg["surf"],
-                                    gasphase=None if cfg["gas"] else "CH4 H2O H2 CO CO2 O2 N2".split())
+    mech = make_mech(pkg, args.config)
     eng = pkg.Engine(mech, device=local)
-    N = args.n or cfg["n"]
-    start, _ = shard.shard_slice(rank, N)
+    if args.scaling == "strong":
+        total = args.n or cfg["n"]
+        start, stop = shard.shard_range(rank, world, total)
+    else:
+        per = args.n or cfg["n"]
+        total = per * world
+        start, stop = shard.shard_slice(rank, per)
+    N = stop - start
     T, Asv, U0 = ensemble.make_inputs(mech, args.config, start, N)
     tf = np.full(N, cfg["tf"])
     dT = torch.from_numpy(T).to(dev)
@@ -100,60 +122,92 @@ def main():
     st = dst.cpu().numpy()
     stats = {k: st[:, i] for i, k in enumerate(pkg.STAT_FIELDS)}
     nbad = int(np.sum(stats["status"] != 0))
+    nbad_all = nbad
+    if world > 1:   # failures summed over ranks (outside the timed region)
+        t_bad = torch.tensor([float(nbad)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t_bad)
+        nbad_all = int(t_bad.item())
     flops = ensemble.algorithmic_flops(mech, stats)
     kernel_ms = float(np.mean(kms))
     achieved = flops / (kernel_ms * 1e-3) / 1e12
+    # algorithmic HBM bytes per launch: inputs (T, Asv, tf, u0[n]) read, u[n] + stats written
+    alg_bytes = N * 8.0 * ((3 + mech.n) + (mech.n + pkg._lib.NSTAT))
 
-    # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
-    # kernel on this workload (bytes per reactor x reactors in this launch); None if absent
-    traffic = None
-    if args.config == "gri" and os.path.exists(args.traffic):
-        with open(args.traffic) as fh:
-            traffic = json.load(fh)["bytes_per_reactor"] * N
+    # measured memory-side bytes per reactor of this kernel at this HEAD (rocprofv3 FETCH_SIZE x2
+    # + WRITE_SIZE passes, scripts/pmc_traffic.py -> profiles/r02_traffic_<config>.json)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", f"r02_traffic_{args.config}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            tj = json.load(fh)
+        traffic = tj["bytes_per_reactor"] * N
+        traffic_src = os.path.relpath(tpath, ROOT)
 
     gather_ms = None
     if world > 1:   # the single result gather over RCCL/xGMI (outside the timed region)
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        shard.gather_ensemble(dU, dst, dist)
+        shard.gather_ensemble(dU, dst, dist, total if args.scaling == "strong" else None)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
 
-    cpu = None
-    parity = None
+    cpu = parity = phases = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(mech, T, Asv, U0, tf, dU.cpu().numpy(), stats["status"], args.cpu_seconds)
+        cpu, parity = cpu_baseline(mech, args.config, T, Asv, U0, tf, dU.cpu().numpy(), stats["status"],
+                                   args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_phase:
+        phases = run_phase_split(args.config)
 
     if rank == 0:
-        total = N * world
         per_step = elapsed / args.steps
+        kernel_s = kernel_ms * 1e-3
+        roof = {"bound": "fp64 valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                "traffic_unit": "B per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, per reactor x N)",
+                "traffic_source": traffic_src, "kernel": eng.kernel_name, "kernel_ms": kernel_ms,
+                "algorithmic_flop_per_launch": flops,
+                "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
+                        "algorithmic_GBs": alg_bytes / kernel_s / 1e9,
+                        "measured_GBs": (traffic / kernel_s / 1e9) if traffic else None,
+                        "peak_GBs": HBM_PEAK_GBS,
+                        "frac_measured": (traffic / kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None}}
+        if phases:
+            # the north_star's rate+Jacobian figure: their FLOPs over the kernel time spent in them
+            f = ensemble.flop_model(mech)
+            rj_flops = float(np.sum(stats["nfe"]) * f["rhs"] + np.sum(stats["nje"]) * f["jac"])
+            share = phases["rhs_share"] + phases["jac_share"]
+            rj = rj_flops / (kernel_s * share) / 1e12 if share > 0 else None
+            roof["rate_jacobian"] = {"achieved": rj, "frac": rj / FP64_PEAK_TFLOPS if rj else None,
+                                     "unit": "TFLOP/s", "flop_per_launch": rj_flops, "kernel_time_share": share,
+                                     "phase_shares": phases, "source": "diagnostic build (libbrhip_diag.so) "
+                                     "per-phase shader clocks on a sample of the same workload"}
+        ok_all = total - nbad_all
         line = {
             "metric": "reactor integrations/sec (CH4 GRI ensemble)" if args.config == "gri"
             else f"reactor integrations/sec ({args.config} ensemble)",
-            "value": total / per_step,
+            # successful integrations only: a reactor that stops with a CVODE failure status is
+            # not counted (the work it did still costs time)
+            "value": ok_all / per_step,
             "unit": "reactors/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": per_step * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (splitmix64 seed 20250711, SURVEY.md 8(d))",
-            "config": {"workload": cfg["name"], "reactors_per_gpu": N, "total_reactors": total,
+            "config": {"workload": cfg["name"], "total_reactors": total, "reactors_rank0": N,
                        "tf_s": cfg["tf"], "rtol": 1e-6, "atol": 1e-10, "parallelism": f"ensemble dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "traffic_unit": "B per launch (PMC, profiles/traffic_gri.json)",
-                         "kernel": eng.kernel_name, "kernel_ms": kernel_ms,
-                         "algorithmic_flop_per_launch": flops},
+            "roofline": roof,
             "cpu_baseline": cpu,
-            "solver": {"failed": nbad, "status_counts": {str(int(k)): int(np.sum(stats["status"] == k))
-                                                         for k in np.unique(stats["status"])}, "mean_steps": float(stats["nsteps"].mean()),
-                       "mean_nfe": float(stats["nfe"].mean()), "mean_nje": float(stats["nje"].mean()),
-                       "mean_nsetups": float(stats["nsetups"].mean())},
-            "parity_vs_oracle_err": parity,
+            "solver": {"failed_all_ranks": nbad_all, "attempted": total, "failed": nbad, "status_counts": {str(int(k)): int(np.sum(stats["status"] == k))
+                                                         for k in np.unique(stats["status"])},
+                       "mean_steps": float(stats["nsteps"].mean()), "mean_nfe": float(stats["nfe"].mean()),
+                       "mean_nje": float(stats["nje"].mean()), "mean_nsetups": float(stats["nsetups"].mean()),
+                       "mean_t_ign": float(np.nanmean(stats["t_ign"])) if np.any(np.isfinite(stats["t_ign"])) else None},
+            "parity_vs_oracle": parity,
             "gather_ms": gather_ms,
         }
         print(json.dumps(line), flush=True)
@@ -161,17 +215,46 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(mech, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
+def run_phase_split(config):
+    """Per-phase kernel-time shares from the diagnostic build, in a child process (its own
+    library instance); a sample of the same workload."""
+    env = dict(os.environ)
+    env["BRHIP_LIB"] = os.path.join(ROOT, "batchreactor.jl_amd", "libbrhip_diag.so")
+    if not os.path.exists(env["BRHIP_LIB"]):
+        return None
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--phase-only", "--config", config],
+                           env=env, capture_output=True, text=True, timeout=300)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception:
+        return None
+
+
+def phase_split(args):
+    import _pkgload
+    pkg = _pkgload.load()
+    from batchreactor_amd import ensemble
+    mech = make_mech(pkg, args.config)
+    N = min(20000, CONFIGS[args.config]["n"])
+    T, Asv, U0 = ensemble.make_inputs(mech, args.config, 0, N)
+    U, st = pkg.Engine(mech).integrate(T, Asv, U0, CONFIGS[args.config]["tf"])
+    clk = float(np.sum(st["cyc_clk"]))
+    out = {f"{ph}_share": float(np.sum(st["cyc_" + ph]) / clk) for ph in ("rhs", "jac", "lu", "sol", "ctl")}
+    out["reactors"] = N
+    print(json.dumps(out))
+
+
+def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
     """The C CPU oracle (CVODE restatement, analytic Jacobian, OpenMP over reactors) on a bounded
-    sample of the same workload; also checks the GPU results of that sample against it."""
+    sample of the same workload, all threads and one thread; also checks the GPU results of that
+    sample against it (per reactor, the metric of tests/test_gpu_parity.py at t = tf)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    cfg = CONFIGS[config]
     lib = os.path.join(ROOT, "tests", "golden", "lib")
-    om = oracle.Mech(os.path.join(lib, "grimech.dat") if mech.nrg and mech.ng > 9 else
-                     (os.path.join(lib, "h2o2.dat") if mech.nrg else None),
-                     os.path.join(lib, "therm.dat"),
-                     os.path.join(lib, "ch4ni.xml") if mech.ns else None,
-                     gas_species=None if mech.nrg else mech.gas_species)
+    om = oracle.Mech(os.path.join(lib, cfg["gas"]) if cfg["gas"] else None, os.path.join(lib, "therm.dat"),
+                     os.path.join(lib, cfg["surf"]) if cfg["surf"] else None,
+                     gas_species=None if cfg["gas"] else mech.gas_species)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 64))
     k = min(threads, len(T))
@@ -183,20 +266,25 @@ def cpu_baseline(mech, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
     t0 = time.perf_counter()
     Uo, sto, bad = om.integrate_batch(T[:k], Asv[:k], U0[:k], tf[:k], analytic_jac=True, nthreads=threads)
     dt = time.perf_counter() - t0
-    # parity metric of tests/test_gpu_parity.py: max |du| / (1e-4 |u| + 100 atol), pass <= 1,
-    # over the reactors both sides integrated successfully
+    k1 = int(max(1, min(k, 0.25 * seconds / max(per, 1e-6))))      # single thread, a quarter of the budget
+    t1 = time.perf_counter()
+    om.integrate_batch(T[:k1], Asv[:k1], U0[:k1], tf[:k1], analytic_jac=True, nthreads=1)
+    dt1 = time.perf_counter() - t1
     ok = np.array([s["status"] == 0 for s in sto]) & (gpu_status[:k] == 0)
     if ok.any():
         err = np.max(np.abs(U_gpu[:k][ok] - Uo[ok]) / (1e-4 * np.abs(Uo[ok]) + 1e-8), axis=1)
-        rel = {"metric": "max_k |u_gpu-u_orc| / (1e-4 |u_orc| + 100 atol) per reactor", "reactors": int(ok.sum()),
-               "failed_either": int((~ok).sum()), "median": float(np.median(err)),
+        rel = {"metric": "max_k |u_gpu-u_orc| / (1e-4 |u_orc| + 100 atol) per reactor at t = tf (post-ignition: "
+                         "rounding-level differences grow through ignition, see tests/test_gpu_parity.py bands)",
+               "reactors": int(ok.sum()), "failed_either": int((~ok).sum()), "median": float(np.median(err)),
                "p99": float(np.percentile(err, 99)), "max": float(err.max()),
-               "frac_le_1": float(np.mean(err <= 1.0)), "frac_le_10": float(np.mean(err <= 10.0))}
+               "frac_le_1": float(np.mean(err <= 1.0)), "frac_le_30": float(np.mean(err <= 30.0))}
     else:
         rel = None
     return ({"value": k / dt, "unit": "reactors/s", "cores": threads, "kind": "port",
-             "sample": f"first {k} reactors of the same synthetic workload, C oracle (oracle/oracle.c, "
-                       f"CVODE restatement, analytic Jacobian), OpenMP {threads} threads, {dt:.1f} s"}, rel)
+             "single_thread_value": k1 / dt1,
+             "sample": f"first {k} reactors of the same synthetic workload ({k1} for the single-thread figure), "
+                       f"C oracle (oracle/oracle.c, CVODE restatement, analytic Jacobian), OpenMP {threads} "
+                       f"threads, {dt:.1f} s; 1 thread {dt1:.1f} s"}, rel)
 
 
 if __name__ == "__main__":

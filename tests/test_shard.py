@@ -39,6 +39,26 @@ def _oracle_run(m, T, Asv, U0):
     return U, S
 
 
+def _rank_strong(rank, world, port, out_dir, total):
+    """strong scaling: `total` reactors split over the ranks (slices differ in length by one)"""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+    import _pkgload
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = _pkgload.load()
+    from batchreactor_amd import shard
+    start, stop = shard.shard_range(rank, world, total)
+    m, (T, Asv, U0) = _inputs(pkg, start, stop - start)
+    U, S = _oracle_run(m, T, Asv, U0)
+    Ug, Sg = shard.gather_ensemble(torch.from_numpy(U), torch.from_numpy(S), dist, total)
+    np.save(os.path.join(out_dir, f"SU{rank}.npy"), Ug.numpy())
+    np.save(os.path.join(out_dir, f"SS{rank}.npy"), Sg.numpy())
+    dist.destroy_process_group()
+
+
 def _rank(rank, world, port, out_dir):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -70,3 +90,29 @@ def test_two_rank_gloo_shard_and_gather(pkg, orc, tmp_path):
         np.testing.assert_array_equal(np.load(tmp_path / f"U{r}.npy"), U)   # same inputs, same order
         np.testing.assert_array_equal(np.load(tmp_path / f"S{r}.npy"), S)
         assert float(np.load(tmp_path / f"t{r}.npy")[0]) == 0.5 + (world - 1)
+
+
+def test_strong_scaling_slices_cover_the_ensemble(pkg):
+    """shard_range: contiguous slices in ensemble order, sizes within one, union = [0, total),
+    for the BASELINE 1e5 ensemble over 1/2/4/8 GPUs and ragged totals."""
+    from batchreactor_amd import shard
+    for total in (100000, 7, 12345, 3):
+        for world in (1, 2, 3, 4, 8):
+            r = [shard.shard_range(k, world, total) for k in range(world)]
+            assert r[0][0] == 0 and r[-1][1] == total
+            assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
+            sizes = [b - a for a, b in r]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_two_rank_gloo_strong_scaling(pkg, orc, tmp_path):
+    """Strong scaling over two gloo ranks with an odd total (slices of 3 and 2 reactors): the
+    gathered ensemble equals a single-process run over the whole range, in order."""
+    world, total = 2, 5
+    mp.start_processes(_rank_strong, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
+                       start_method="spawn")
+    m, (T, Asv, U0) = _inputs(pkg, 0, total)
+    U, S = _oracle_run(m, T, Asv, U0)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"SU{r}.npy"), U)
+        np.testing.assert_array_equal(np.load(tmp_path / f"SS{r}.npy"), S)
