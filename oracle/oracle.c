@@ -939,9 +939,13 @@ static void dq_jac(cv_t* cv, const double* y, const double* fy, double* Jc /* co
     double* yy = cv->tempv; /* scratch copy */
     for (int i = 0; i < n; ++i) yy[i] = y[i];
     double* ft = (double*)malloc(sizeof(double) * (size_t)n);
+    /* test hook (scripts/diag_spread.py): a relative perturbation of the DQ increments, the size of
+       the rounding differences between two implementations of cvLsDenseDQJac */
+    static double jitter = -1.0;
+    if (jitter < 0.0) { const char* e = getenv("ORC_DQ_JITTER"); jitter = e ? atof(e) : 0.0; }
     for (int j = 0; j < n; ++j) {
         double ys = yy[j];
-        double inc = fmax(srur * fabs(ys), minInc / cv->ewt[j]);
+        double inc = fmax(srur * fabs(ys), minInc / cv->ewt[j]) * (1.0 + ((j & 1) ? jitter : -jitter));
         yy[j] += inc;
         fcall(cv, yy, ft);
         cv->nfeDQ++;

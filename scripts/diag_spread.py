@@ -26,3 +26,5 @@ for i in range(N):
     if sa['t_ign']==sa['t_ign']: dti.append(abs(sb['t_ign']-sa['t_ign'])/max(sa['ign_dt'],sb['ign_dt']))
 W=np.array(W); S=np.array(S)
 print(case,'aj',aj,'band max',W.max(0),'p99',np.percentile(W,99,axis=0),'steps rel max',np.abs(S).max(),'p90',np.percentile(np.abs(S),90),'sum',S.mean(),'tign/dt max',max(dti) if dti else None)
+# with ORC_DQ_JITTER=<eps> in the environment the perturbed run also perturbs the DQ increments:
+#   ORC_DQ_JITTER=1e-15 python scripts/diag_spread.py h2o2 256 0
