@@ -36,7 +36,7 @@ NSTAT = 20
 
 
 EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info", "br_mech_engine", "br_mech_launch_info",
-           "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_traced", "br_integrate_dev",
+           "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev",
            "br_last_kernel_ms", "br_debug_lu_solve"]
 
 _lib = None
@@ -65,11 +65,12 @@ def lib():
     L.br_integrate.argtypes = [vp, C.c_int, dp, dp, dp, dp, C.POINTER(Opts), dp]
     L.br_integrate_traced.argtypes = [vp, C.c_int, dp, dp, dp, dp, C.POINTER(Opts), dp, dp]
     L.br_integrate_dev.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.POINTER(Opts), vp, vp]
+    L.br_integrate_multi.argtypes = [C.POINTER(vp), C.c_int, C.c_int, dp, dp, dp, dp, C.POINTER(Opts), dp]
     L.br_last_kernel_ms.argtypes = [vp, dp]
     L.br_debug_lu_solve.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, ip]
     L.br_debug_lu_solve.restype = C.c_int
     for f in ("br_mech_create", "br_mech_destroy", "br_mech_info", "br_rates", "br_rhs", "br_jacobian",
-              "br_integrate", "br_integrate_traced", "br_integrate_dev", "br_last_kernel_ms"):
+              "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev", "br_last_kernel_ms"):
         getattr(L, f).restype = C.c_int
     _lib = L
     return L

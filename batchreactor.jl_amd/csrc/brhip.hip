@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/brhip.h"
@@ -50,6 +51,9 @@ struct KOpts {
                               // wavefront engine (restart from u0); >= max_steps disables
     const int* rid_list;      // k_integrate: integrate reactors rid_list[0 .. min(*rid_count, N)) only
     const int* rid_count;
+    const double* rid_t0;     // with rid_list: start time of list entry i (a deferred lane reactor
+                              // continues from its last accepted state U[rid] at rid_t0[i]: CVODE
+                              // restart there) and its counters so far are in stats[rid]
     int* work;                // k_integrate: persistent waves take reactor indices from this
                               // counter (nullptr: one reactor per wave, index = wave slot)
 };
@@ -919,19 +923,33 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     C->delp = 0.0; C->hprime = 0.0; C->hscale = 0.0; C->eta = 1.0; C->etamax = ETAMX1; C->acnrm = 0.0;
     C->saved_tq5 = 0.0; C->saved_t = 0.0; C->tol = 0.0; C->hg = 0.0; C->hub = 0.0; C->hlb = 0.0; C->hnew = 0.0;
     C->tstop = tfv[rid];
+    const double t0 = o.rid_t0 ? uni(o.rid_t0[idx]) : 0.0;   // > 0: continue a deferred lane reactor
+    C->tn = t0;
     C->ulimit = o.ufac > 0.0 ? o.ufac * uni(wave_sum(su)) : INFINITY;
     C->q = 1; C->qprime = 1; C->L = 2; C->qwait = 2;
     C->nst = 0; C->nfe = 0; C->nsetups = 0; C->nje = 0; C->nni = 0; C->ncfn = 0; C->netf = 0; C->nstlp = 0;
     C->nstlj = 0; C->ncf = 0; C->nef = 0; C->nstloc = 0; C->status = 0; C->m_it = 0; C->convfail = 0;
     C->count1 = 0; C->phase = PH_F0; C->callSetup = 0; C->jbad = 0; C->jcur_nls = 0; C->hnewOK = 0; C->newj = 0;
     C->p_last = 0.0;
-    C->iout = 0; C->ign_t = 0.0; C->ign_rate = -INFINITY; C->t_ign = NAN; C->ign_x = 0.0; C->ign_dt = NAN;
+    C->iout = 0; C->ign_t = t0; C->ign_rate = -INFINITY; C->t_ign = NAN; C->ign_x = 0.0; C->ign_dt = NAN;
     if (o.ign >= 0) C->ign_x = uni(mole_frac_of<CPL>(u0, lane, o.ign));
-    if (o.nout) {                                           // outputs at t <= 0: the initial state
-        int io = 0;
-        while (io < o.nout && !(o.tout[io] > 0.0)) {
+    // counters and ignition marker of the lane pass (deferred reactors) to continue from
+    double st_in[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (o.rid_t0 && stats) {
 #pragma unroll
-            FOR_S if (CS < n) o.yout[((size_t)rid * o.nout + io) * n + CS] = u0[s];
+        for (int k = 0; k < 7; ++k) st_in[k] = uni(stats[(size_t)rid * BR_NSTAT + k]);
+        if (o.ign >= 0) {
+            C->ign_rate = uni(stats[(size_t)rid * BR_NSTAT + 17]);
+            C->t_ign = uni(stats[(size_t)rid * BR_NSTAT + 16]);
+            C->ign_dt = uni(stats[(size_t)rid * BR_NSTAT + 18]);
+        }
+    }
+    if (o.nout) {                                           // outputs at t <= t0: the initial state
+        int io = 0;
+        while (io < o.nout && !(o.tout[io] > t0)) {
+            if (!o.rid_t0)                                  // (a continued reactor wrote them already)
+#pragma unroll
+                FOR_S if (CS < n) o.yout[((size_t)rid * o.nout + io) * n + CS] = u0[s];
             ++io;
         }
         C->iout = io;
@@ -1005,9 +1023,9 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     }
     if (stats && lane == 0) {
         double* st = stats + (size_t)rid * BR_NSTAT;
-        st[0] = (double)ui(C->nst); st[1] = (double)ui(C->nfe); st[2] = (double)ui(C->nje);
-        st[3] = (double)ui(C->nsetups); st[4] = (double)ui(C->nni); st[5] = (double)ui(C->ncfn);
-        st[6] = (double)ui(C->netf); st[7] = (double)status;
+        st[0] = st_in[0] + ui(C->nst); st[1] = st_in[1] + ui(C->nfe); st[2] = st_in[2] + ui(C->nje);
+        st[3] = st_in[3] + ui(C->nsetups); st[4] = st_in[4] + ui(C->nni); st[5] = st_in[5] + ui(C->ncfn);
+        st[6] = st_in[6] + ui(C->netf); st[7] = (double)status;
         st[8] = (double)(wall_clock64() - cyc0);
 #if BR_PHASE_CLOCKS
         st[9] = (double)cyc_rhs; st[10] = (double)cyc_jac; st[11] = (double)cyc_lu; st[12] = (double)cyc_sol;
@@ -1138,6 +1156,7 @@ struct br_mech {
     size_t lws_bytes = 0;
     int* queue = nullptr;      // work counter
     int* wq = nullptr;         // k_integrate work counter
+    double* defer_t0 = nullptr; // start time of each deferred lane reactor (DEFER_CAP)
     int ncu = 0;
 };
 
@@ -1456,6 +1475,7 @@ int br_mech_destroy(br_mech* m) {
     if (m->lws) hipFree(m->lws);
     if (m->queue) hipFree(m->queue);
     if (m->wq) hipFree(m->wq);
+    if (m->defer_t0) hipFree(m->defer_t0);
     if (m->ev0) hipEventDestroy(m->ev0);
     if (m->ev1) hipEventDestroy(m->ev1);
     delete m;
@@ -1589,6 +1609,7 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.defer_steps = o.max_steps;
     o.rid_list = nullptr;
     o.rid_count = nullptr;
+    o.rid_t0 = nullptr;
     o.work = nullptr;
     hipStream_t s = (hipStream_t)stream;
     const char* eng = getenv("BRHIP_ENGINE");   // "wave" forces the wave-per-reactor engine
@@ -1613,21 +1634,23 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
         int rc = ensure_jws(m, cap);
         if (rc) return rc;
         if (!m->queue) HIPCHK(hipMalloc((void**)&m->queue, (2 + DEFER_CAP) * sizeof(int)));
+        if (!m->defer_t0) HIPCHK(hipMalloc((void**)&m->defer_t0, DEFER_CAP * sizeof(double)));
         HIPCHK(hipMemsetAsync(m->queue, 0, 2 * sizeof(int), s));
         HIPCHK(hipEventRecord(m->ev0, s));
         if (NM == 9) {
             HIPCHK(hipFuncSetAttribute((const void*)k_lane<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem));
-            hipLaunchKernelGGL(k_lane<9>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue, cap);
+            hipLaunchKernelGGL(k_lane<9>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue, m->defer_t0, cap);
         } else {
             HIPCHK(hipFuncSetAttribute((const void*)k_lane<12>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lane_shmem));
-            hipLaunchKernelGGL(k_lane<12>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue, cap);
+            hipLaunchKernelGGL(k_lane<12>, dim3(blocks), dim3(64), m->lane_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->lws, m->queue, m->defer_t0, cap);
         }
         HIPCHK(hipGetLastError());
-        if (o.defer_steps < o.max_steps) {   // the deferred reactors, from u0, on the wavefront engine
+        if (o.defer_steps < o.max_steps) {   // the deferred reactors continue on the wavefront engine
             KOpts o2 = o;
             o2.defer_steps = o.max_steps;
             o2.rid_list = m->queue + 2;
             o2.rid_count = m->queue + 1;
+            o2.rid_t0 = m->defer_t0;
             const int rpb = m->rpb;
             HIPCHK(hipFuncSetAttribute((const void*)k_integrate<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem));
             hipLaunchKernelGGL(k_integrate<16>, dim3((cap + rpb - 1) / rpb), dim3(64 * rpb), m->shmem, s, m->dm, cap, rpb, dT,
@@ -1746,6 +1769,37 @@ int br_integrate(br_mech* m, int N, const double* T, const double* Asv, double* 
 int br_integrate_traced(br_mech* m, int N, const double* T, const double* Asv, double* u, const double* tf,
                         const br_opts* opts, br_stats* stats, double* trace) {
     return integrate_host(m, N, T, Asv, u, tf, opts, stats, trace);
+}
+
+int br_integrate_multi(br_mech* const* mechs, int ndev, int N, const double* T, const double* Asv, double* u,
+                       const double* tf, const br_opts* opts, br_stats* stats) {
+    if (!mechs || ndev < 1 || N < 0 || !T || !u || !tf) return fail(BR_ERR_INPUT, "bad argument");
+    for (int d = 0; d < ndev; ++d) {
+        if (!mechs[d] || mechs[d]->n != mechs[0]->n) return fail(BR_ERR_INPUT, "handles differ in size");
+        for (int e = 0; e < d; ++e)
+            if (mechs[e] == mechs[d]) return fail(BR_ERR_INPUT, "one handle per shard (handles hold workspaces)");
+    }
+    const int n = mechs[0]->n;
+    const int nout = (opts && opts->nout > 0 && opts->tout && opts->yout) ? opts->nout : 0;
+    std::vector<int> rc(ndev, 0);
+    std::vector<std::string> msg(ndev);
+    std::vector<std::thread> th;
+    const int base = N / ndev, extra = N % ndev;
+    for (int d = 0; d < ndev; ++d) {
+        const int start = d * base + std::min(d, extra), cnt = base + (d < extra ? 1 : 0);
+        th.emplace_back([&, d, start, cnt]() {
+            br_opts od{};
+            if (opts) od = *opts;
+            if (nout) od.yout = opts->yout + (size_t)start * nout * n;
+            rc[d] = integrate_host(mechs[d], cnt, T + start, Asv ? Asv + start : nullptr, u + (size_t)start * n,
+                                   tf + start, opts ? &od : nullptr, stats ? stats + start : nullptr, nullptr);
+            if (rc[d]) msg[d] = g_err;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int d = 0; d < ndev; ++d)
+        if (rc[d]) return fail(rc[d], "shard " + std::to_string(d) + ": " + msg[d]);
+    return 0;
 }
 
 }  // extern "C"

@@ -1077,8 +1077,10 @@ __device__ __forceinline__ void lane_jac(const LaneLay& LL, const double* Lp, co
 template <int NM>
 __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __restrict__ Tv, double* __restrict__ U,
                                              const double* __restrict__ tfv, KOpts o, double* __restrict__ stats,
-                                             double* __restrict__ Jg, int* __restrict__ queue, int defer_cap) {
-    // queue[0]: next reactor; queue[1]: deferred count; queue[2 ..]: deferred reactor ids
+                                             double* __restrict__ Jg, int* __restrict__ queue, double* __restrict__ defer_t0,
+                                             int defer_cap) {
+    // queue[0]: next reactor; queue[1]: deferred count; queue[2 ..]: deferred reactor ids;
+    // defer_t0[i]: the time of deferred entry i's last accepted state
     const int lane = threadIdx.x;
     const int n = MF(n);
     const LaneLay LL = lane_lay(NM, n, MF(nset), MF(nrg), MF(nfo));
@@ -1201,8 +1203,17 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
         LACC(k_ctl, t5);
         if (act == A_DONE && c.status == ST_DEFER) {
             const int di = atomicAdd(queue + 1, 1);
-            if (di < defer_cap) {
-                queue[2 + di] = rid;                         // U[rid] still holds u0
+            if (di < defer_cap) {                            // hand over the last accepted state
+                queue[2 + di] = rid;
+                defer_t0[di] = c.tn;
+#pragma unroll
+                for (int i = 0; i < NM; ++i) if (i < n) U[(size_t)rid * n + i] = z.z0[i];
+                if (stats) {                                 // counters so far (the wave pass adds its own)
+                    double* st = stats + (size_t)rid * BR_NSTAT;
+                    st[0] = (double)c.nst; st[1] = (double)c.nfe; st[2] = (double)c.nje; st[3] = (double)c.nsetups;
+                    st[4] = (double)c.nni; st[5] = (double)c.ncfn; st[6] = (double)c.netf;
+                    st[16] = c.t_ign; st[17] = c.ign_rate; st[18] = c.ign_dt;
+                }
                 has = false;
             } else {                                         // no room: keep integrating here
                 c.status = 0;

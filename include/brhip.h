@@ -160,6 +160,16 @@ int br_integrate(br_mech* m, int N, const double* T, const double* Asv, double* 
 int br_integrate_traced(br_mech* m, int N, const double* T, const double* Asv, double* u,
                         const double* tf, const br_opts* opts, br_stats* stats, double* trace);
 
+/* multi-GPU ensemble: N reactors split into ndev contiguous slices (sizes
+ * differ by at most one), slice d integrated on mechs[d] -- one handle per GPU, created with
+ * br_mech_create(desc, device d, ...) -- concurrently (one host thread per handle), results
+ * written back into the caller's host arrays in ensemble order. No inter-GPU traffic: every
+ * slice is copied straight back to host memory. Arguments as br_integrate (opts->yout, when set,
+ * is [N][nout][n] for the whole ensemble). Replaces running the reference's solve() once per
+ * reactor (src/BatchReactor.jl:138-141). */
+int br_integrate_multi(br_mech* const* mechs, int ndev, int N, const double* T, const double* Asv, double* u,
+                       const double* tf, const br_opts* opts, br_stats* stats);
+
 /* device-buffer entry point: all pointers are device memory on m's device; `stream` is a
  * hipStream_t (NULL = default stream). Asynchronous: returns after the launch. Calls on one
  * handle share its workspaces (work counter, Jacobian / LU slots, timing events): they must be
