@@ -19,6 +19,9 @@
 #include "../../include/brhip.h"
 #include "brhip_device.hpp"
 
+#ifndef BR_ASM_MARKS
+#define BR_ASM_MARKS 0
+#endif
 #ifndef BR_PHASE_CLOCKS
 #define BR_PHASE_CLOCKS 0   // per-phase shader-clock counters in br_stats (diagnostic build: libbrhip_diag.so)
 #endif
@@ -120,8 +123,12 @@ __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { retu
 // matrix columns hold 64 * CPL rows (CPL = 2 for nmax > 64)
 __host__ __device__ inline int col_rows(int nmax) { return nmax > 64 ? 128 : 64; }
 __host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * col_rows(nmax); }   // M, D
-__host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
+// [J | LU factors | Jacobian scratch (2 per gas reaction) | RXD: {kf, kr} per gas reaction]
+__host__ __device__ inline size_t rxd_ws_off(int nmax, int nrg) {
     return (size_t)nmax * col_rows(nmax) + lu_ws_doubles(nmax) + (((size_t)2 * nrg + 63) / 64) * 64;
+}
+__host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
+    return rxd_ws_off(nmax, nrg) + (((size_t)2 * nrg + 63) / 64) * 64;
 }
 
 struct WaveCtx {
@@ -130,8 +137,9 @@ struct WaveCtx {
     char* rbase;   // this wave's reactor block
     RView R;
 };
-template <int CPL>
-__device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rpb) {
+// ws: the global workspace, NMAX-instance slots (slot = wave index rid)
+template <int CPL, int NMAX>
+__device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rpb, double* ws) {
     WaveCtx w;
     w.wave = uni((int)(threadIdx.x >> 6));   // uniform per wave: scalar addressing of its reactor
     w.lane = threadIdx.x & 63;
@@ -139,7 +147,8 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
     stage_tables(M, smem);
     w.tb = tab_view<CPL>(smem, M);
     w.rbase = smem + M.img_bytes + (size_t)w.wave * reactor_bytes(M);
-    w.R = rview<CPL>(w.rbase + CTL_BYTES + vec_bytes(CPL), M);
+    w.R = rview<CPL>(w.rbase + CTL_BYTES + vec_bytes(CPL), M,
+                     launder(ws + (size_t)w.rid * ws_doubles(NMAX, M.nrg) + rxd_ws_off(NMAX, M.nrg)));
     return w;
 }
 
@@ -847,16 +856,25 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
 #ifndef BR_WPE
 #define BR_WPE 2
 #endif
+#ifndef BR_ACC_NMAX
+#define BR_ACC_NMAX 0   // largest NMAX whose LU factors live in AGPRs (0: all in global memory)
+#endif
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
 // n <= 64 keeps 256-thread workgroups (2 x 4 or 4 x 2 reactors, 8 waves/CU, VGPR-limited)
 __host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 8 : 4; }
+constexpr size_t LDS_PER_CU = 160 * 1024, LDS_GRANULE = 1280;   // gfx950 (granule: conservative)
 #ifndef BR_WPE32
 #define BR_WPE32 3   // n <= 32 (surface-only): 3 waves/SIMD, 12 waves/CU (LDS allows it; 130k -> 156k/s)
 #endif
 // minimum waves per SIMD the register allocator must allow, per instance
-__host__ __device__ constexpr int br_wpe(int nmax) { return nmax == 32 ? BR_WPE32 : BR_WPE; }
+#ifndef BR_WPE56
+#define BR_WPE56 3   // n in 33..64 (GRI): 3 waves/SIMD (<= 168 VGPRs; LDS allows 12 reactors/CU)
+#endif
+__host__ __device__ constexpr int br_wpe(int nmax) {
+    return nmax == 32 ? BR_WPE32 : (nmax == 56 || nmax == 64) ? BR_WPE56 : BR_WPE;
+}
 template <int NMAX>
 __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_per_eu(br_wpe(NMAX), 8))) void k_integrate(
     DevMech M, int N, int rpb, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
@@ -865,7 +883,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     constexpr int CPL = NMAX > 64 ? 2 : 1;   // components per lane
     constexpr int VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL, NMAX>(M, smem_raw, rpb, Jws);
     // Reactor indices: with o.work every wave of the (resident-sized) grid keeps taking the next
     // index from the counter until the list is drained, so a wave whose reactor finishes early
     // starts another instead of idling until the slowest reactor of its workgroup is done; the
@@ -955,7 +973,10 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         C->iout = io;
     }
 
-#if BR_PHASE_CLOCKS
+#if BR_ASM_MARKS   // analysis builds: phase markers in the ISA listing (they are scheduling barriers)
+#define BR_CLK(v) asm volatile("; BR_PHASE_BEGIN " #v)
+#define BR_ACC(acc, v) asm volatile("; BR_PHASE_END " #acc)
+#elif BR_PHASE_CLOCKS
     unsigned long long cyc_rhs = 0, cyc_jac = 0, cyc_lu = 0, cyc_sol = 0, cyc_ctl = 0;
     const unsigned long long clk0 = clock64();
 #define BR_CLK(v) const unsigned long long v = clock64()
@@ -968,6 +989,10 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     int perm[CPL];
 #pragma unroll
     FOR_S perm[s] = CS;
+    // LU factors resident in AGPRs across the Newton iterations that reuse them (CPL = 1, NMAX <=
+    // BR_ACC_NMAX); otherwise in the per-slot global workspace
+    constexpr bool ACCF = (CPL == 1) && (NMAX <= BR_ACC_NMAX);
+    AccFac<ACCF ? NMAX : 1> af;
     LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // LU scratch (CPL = 2): the production sums are idle then
     double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
     for (;;) {
@@ -993,7 +1018,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
+            if constexpr (ACCF) lu_fail = lu_factor<NMAX, true>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], &af);
+            else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
         }
@@ -1002,7 +1028,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         FOR_S delta[s] = 0.0;
         if (!lu_fail) {
             BR_CLK(c0);
-            if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0]);
+            if constexpr (ACCF) delta[0] = lu_solve_acc<NMAX>(af, n, lane, perm[0], b[0]);
+            else if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0]);
             else {
                 lu_solve2<NMAX>(LUsave, scr, n, lane, perm, b);
                 delta[0] = b[0];
@@ -1045,10 +1072,10 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
 // ------------------------------------------------------------------------------------
 template <int CPL>
 __global__ __launch_bounds__(256) void k_rates(DevMech M, int N, int rpb, const double* Tv, const double* pv,
-                                               const double* X, const double* TH, double* W_, double* SD) {
+                                               const double* X, const double* TH, double* W_, double* SD, double* Jws) {
     typedef Lay<CPL> L;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL, CPL == 2 ? 72 : 64>(M, smem_raw, rpb, Jws);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
@@ -1069,7 +1096,7 @@ __global__ __launch_bounds__(256) void k_rates(DevMech M, int N, int rpb, const 
     wave_sync();
     third_body_sets<CPL>(M, W.tb, S.sp, Ctot, lane);
     wave_sync();
-    production<CPL>(M, W.tb, S, R_GAS * T, lane);
+    production<CPL>(M, W.tb, S, R_GAS * T, lane, rx_prefetch(S, lane));
     wave_sync();
 #pragma unroll
     FOR_S {
@@ -1083,9 +1110,9 @@ __global__ __launch_bounds__(256) void k_rates(DevMech M, int N, int rpb, const 
 
 template <int CPL>
 __global__ __launch_bounds__(256) void k_rhs(DevMech M, int N, int rpb, const double* Tv, const double* Asvv,
-                                             const double* U, double* DU) {
+                                             const double* U, double* DU, double* Jws) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL, CPL == 2 ? 72 : 64>(M, smem_raw, rpb, Jws);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
@@ -1107,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
                                              const double* U, double* J, double* Jws) {
     constexpr int CPL = NMAX > 64 ? 2 : 1, VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const WaveCtx W = wave_ctx<CPL>(M, smem_raw, rpb);
+    const WaveCtx W = wave_ctx<CPL, NMAX>(M, smem_raw, rpb, Jws);
     const int rid = W.rid;
     if (rid >= N) return;
     const int lane = W.lane;
@@ -1432,10 +1459,13 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     int best = 0, best_w = 0;
     for (int rpb = 1; rpb <= br_maxrpb(m->nmax); ++rpb) {
         const size_t b = wg_lds_bytes(M, rpb);
-        if (b > 160 * 1024) break;
+        if (b > LDS_PER_CU) break;
         if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) != hipSuccess) break;
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 64 * rpb, b) != hipSuccess) break;
+        // the calculator ignores the LDS allocation granule: 3 x 54.5 KB workgroups were reported
+        // resident but only 2 were (measured: 6 of 9 waves/CU); count whole granules per CU
+        nb = std::min(nb, (int)(LDS_PER_CU / ((b + LDS_GRANULE - 1) / LDS_GRANULE * LDS_GRANULE)));
         if (nb * rpb > best_w) { best_w = nb * rpb; best = rpb; }
     }
     if (best_w == 0) { br_mech_destroy(m); return fail(BR_ERR_UNSUPPORTED, "mechanism too large for LDS"); }
@@ -1510,6 +1540,8 @@ int br_rates(br_mech* m, int N, const double* T, const double* p, const double* 
     const size_t b_in = (size_t)N * (2 + ng + ns), b_out = (size_t)N * (ng + n);
     int rc = ensure_ws(m, (b_in + b_out) * sizeof(double));
     if (rc) return rc;
+    rc = ensure_jws(m, N);   // per-reactor slots: {kf, kr} per gas reaction
+    if (rc) return rc;
     double* dT = (double*)m->ws;
     double* dp = dT + N;
     double* dx = dp + N;
@@ -1523,10 +1555,10 @@ int br_rates(br_mech* m, int N, const double* T, const double* p, const double* 
     else if (ns) HIPCHK(hipMemset(dth, 0, (size_t)N * ns * sizeof(double)));
     if (m->dm.cpl == 2) {
         HIPCHK(hipFuncSetAttribute((const void*)k_rates<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-        hipLaunchKernelGGL(k_rates<2>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds);
+        hipLaunchKernelGGL(k_rates<2>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds, m->jws);
     } else {
         HIPCHK(hipFuncSetAttribute((const void*)k_rates<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-        hipLaunchKernelGGL(k_rates<1>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds);
+        hipLaunchKernelGGL(k_rates<1>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, dp, dx, ns ? dth : nullptr, dw, ds, m->jws);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(wdot, dw, (size_t)N * ng * sizeof(double), hipMemcpyDeviceToHost));
@@ -1541,6 +1573,8 @@ int br_rhs(br_mech* m, int N, const double* T, const double* Asv, const double* 
     const int n = m->n;
     int rc = ensure_ws(m, ((size_t)N * (2 + 2 * n)) * sizeof(double));
     if (rc) return rc;
+    rc = ensure_jws(m, N);   // per-reactor slots: {kf, kr} per gas reaction
+    if (rc) return rc;
     double* dT = (double*)m->ws;
     double* dA = dT + N;
     double* du_ = dA + N;
@@ -1550,10 +1584,10 @@ int br_rhs(br_mech* m, int N, const double* T, const double* Asv, const double* 
     HIPCHK(hipMemcpy(du_, u, (size_t)N * n * sizeof(double), hipMemcpyHostToDevice));
     if (m->dm.cpl == 2) {
         HIPCHK(hipFuncSetAttribute((const void*)k_rhs<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-        hipLaunchKernelGGL(k_rhs<2>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu);
+        hipLaunchKernelGGL(k_rhs<2>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu, m->jws);
     } else {
         HIPCHK(hipFuncSetAttribute((const void*)k_rhs<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->shmem1));
-        hipLaunchKernelGGL(k_rhs<1>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu);
+        hipLaunchKernelGGL(k_rhs<1>, dim3(N), dim3(64), m->shmem1, 0, m->dm, N, 1, dT, Asv ? dA : nullptr, du_, ddu, m->jws);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(du, ddu, (size_t)N * n * sizeof(double), hipMemcpyDeviceToHost));

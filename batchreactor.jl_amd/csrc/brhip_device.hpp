@@ -9,8 +9,9 @@
 //      SX records (48 B / surface reaction) | SXE (4 doubles / surface reaction: coverage eps) |
 //      TBE third-body entries (16 B: species, eff-1)
 //  * per reactor block: [Ctl][V: Nordsieck + work vectors][SP: conc | accw | accs (64 each)]
-//      [RXD: {kf, kr} per gas reaction][FOD: {k0, log10 Fcent, c, n} per falloff reaction]
-//      [SKD: {k, k*exp(cov)} per surface reaction]
+//      [FOD: {k0, log10 Fcent, c, n} per falloff reaction][SKD: {k, k*exp(cov)} per surface reaction]
+//  * RXD: {kf, kr} per gas reaction, in the wave's global workspace slot (5.2 KB for GRI: kept
+//    out of LDS so 12 reactors fit a CU instead of 8), prefetched at the start of each RHS
 //  * T-dependent rate constants (RXD/FOD/SKD) are computed once per reactor: T is a per-reactor
 //    constant (ConstantParams, src/BatchReactor.jl:14-17).
 // Reactions are evaluated lane-parallel (reaction r on lane r mod 64); production rates are
@@ -37,8 +38,8 @@ struct DevMech {
     int img_bytes;                // multiple of 16
     int sx_off, sxe_off, tbe_off; // byte offsets in the image
     int tbs_off;                  // third-body efficiency sets: one word (start | count << 20) each
-    int fod_off, skd_off;         // byte offsets of FOD / SKD from the reactor's RXD base
-    int rblock_bytes;             // per-reactor LDS bytes from SP start (SP + RXD + FOD + SKD)
+    int fod_off, skd_off;         // byte offsets of FOD / SKD from the end of the species block
+    int rblock_bytes;             // per-reactor LDS bytes from SP start (SP + FOD + SKD)
     // init only (T-dependent constants)
     const double* nasa;           // [ng][15]: Tmid, a_hi[7], a_lo[7]
     const double* g_par;          // [nrg][4]: A (SI), beta, Ea/R, Kc scale
@@ -197,20 +198,20 @@ __device__ __forceinline__ int launder_v(int v) {
 // ------------------------------------------------------------------------------------
 struct RView {
     double* sp;    // species block: conc[k] = sp[CONC+k], accw, accs, mc (see Lay)
-    double* rxd;   // kf = rxd[2r], kr = rxd[2r+1]
+    BR_GLOBAL double* rxd;   // kf = rxd[2r], kr = rxd[2r+1] (global workspace slot)
     double* fod;   // k0, log10 Fcent, c, n per falloff reaction
     double* skd;   // k(T), k*exp(-sum eps theta/RT) (Jacobian) per surface reaction
 };
-__host__ __device__ inline int fod_off_bytes(int nrg) { return (16 * nrg + 15) & ~15; }
+__host__ __device__ inline int fod_off_bytes(int /*nrg*/) { return 0; }   // RXD is in global memory
 __host__ __device__ inline int skd_off_bytes(int nrg, int nfo) { return fod_off_bytes(nrg) + 32 * nfo; }
 __host__ __device__ inline int rblock_bytes(int nrg, int nfo, int nrs, int cpl) {
     return (cpl == 2 ? Lay<2>::BYTES : Lay<1>::BYTES) + skd_off_bytes(nrg, nfo) + 16 * nrs;
 }
 template <int CPL>
-__device__ __forceinline__ RView rview(char* spbase, const DevMech& /*M*/) {
+__device__ __forceinline__ RView rview(char* spbase, const DevMech& /*M*/, BR_GLOBAL double* rxd) {
     RView r;
     r.sp = reinterpret_cast<double*>(spbase);
-    r.rxd = reinterpret_cast<double*>(spbase + Lay<CPL>::BYTES);
+    r.rxd = rxd;
     r.fod = reinterpret_cast<double*>(spbase + Lay<CPL>::BYTES + MF(fod_off));
     r.skd = reinterpret_cast<double*>(spbase + Lay<CPL>::BYTES + MF(skd_off));
     return r;
@@ -300,6 +301,10 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
         else k = sp[0] * pow(T, sp[1]) * exp(-sp[2] / RT);
         R.skd[2 * r] = k;
     }
+    // the RXD stores reach L2 and this CU's L1 is invalidated before any lane reads the slot
+    // (it held the previous reactor's constants)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     wave_sync();
 }
 
@@ -358,18 +363,33 @@ __device__ __forceinline__ void third_body_sets(const DevMech& M, const Tab& tb_
 
 // rates of progress, accumulated straight into the per-species production sums:
 // accw[k] += nu_kr q_r (gas reactions), accs[k] += nu_kr q_r (surface reactions)
+// the {kf, kr} pairs of a lane's first two gas reactions (lane, lane + 64), issued at the start of
+// the RHS so their global-memory latency overlaps the concentration and third-body setup
+struct KPre {
+    double2 a, b;
+};
+__device__ __forceinline__ double2 kpair(const BR_GLOBAL double* rxd, int r) {
+    return make_double2(rxd[2 * r], rxd[2 * r + 1]);   // one 16-byte load
+}
+__device__ __forceinline__ KPre rx_prefetch(const RView& R, int lane) {
+    const int nrg = MF(nrg);
+    KPre k;
+    k.a = kpair(R.rxd, lane < nrg ? lane : 0);
+    k.b = kpair(R.rxd, lane + WAVE < nrg ? lane + WAVE : 0);
+    return k;
+}
 template <int CPL>
-__device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, const RView& R_, double RT, int lane) {
+__device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, const RView& R_, double RT, int lane,
+                                           KPre kp) {
     typedef Lay<CPL> L;
     const Tab tb = tab_view<CPL>(br_lds, M);
-    const RView R = rview<CPL>((char*)R_.sp, M);
+    const RView R = R_;
     const bool xm = (MF(conv) & 2) != 0;
     const double* conc = R.sp + L::CONC;
     double* accw = R.sp + L::ACCW;
     double* accs = R.sp + L::ACCS;
     // net rate of progress of gas reaction r (mass action x third body / falloff)
-    auto rate = [&](int r, const uint4& ra) -> double {
-        const double2 k = *reinterpret_cast<const double2*>(R.rxd + 2 * r);
+    auto rate = [&](int r, const uint4& ra, const double2 k) -> double {
         const uint32_t info = ra.z;
         const int tbk = gi_tb(info);
         // branch-free mass-action products: unused slots point at conc[L::ONE] = 1; mechanisms
@@ -390,19 +410,24 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
         }
         return D;
     };
-    // two reactions per lane and iteration (r and r + 64): their LDS gather chains overlap
+    // two reactions per lane and iteration (r and r + 64): their LDS gather chains overlap; the
+    // next iteration's {kf, kr} loads are issued one iteration ahead
     const int nrg = MF(nrg);
+    double2 kn0 = kp.a, kn1 = kp.b;
 #pragma unroll 1
     for (int r = lane; r < nrg; r += 2 * WAVE) {
         const int r1 = r + WAVE;
         const bool has1 = r1 < nrg;
         const int q1 = has1 ? r1 : r;
+        const double2 k0 = kn0, k1 = has1 ? kn1 : kn0;
+        if (r + 2 * WAVE < nrg) kn0 = kpair(R.rxd, r + 2 * WAVE);
+        if (r + 3 * WAVE < nrg) kn1 = kpair(R.rxd, r + 3 * WAVE);
         const uint4 ra0 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
         const uint4 rb0 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
         const uint4 ra1 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * q1);
         const uint4 rb1 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * q1 + 4);
-        const double D0 = rate(r, ra0);
-        const double D1 = rate(q1, ra1);
+        const double D0 = rate(r, ra0, k0);
+        const double D1 = rate(q1, ra1, k1);
         scatter(accw, rb0.x, rb0.y, rb0.z, D0);
         if (has1) scatter(accw, rb1.x, rb1.y, rb1.z, D1);
     }
@@ -434,7 +459,8 @@ __device__ __forceinline__ void rhs(const DevMech& M, const Tab& tb_, const RVie
                                     double (&du)[CPL]) {
     typedef Lay<CPL> L;
     const Tab tb = tab_view<CPL>(br_lds, M);
-    const RView R = rview<CPL>((char*)R_.sp, M);
+    const RView R = R_;
+    const KPre kp = rx_prefetch(R, lane);
     const int ng = MF(ng), n = MF(n);
     // Y = u/rho, x = (Y/M)/sum(Y/M), p = rho R T / Mbar (:326-338 / :349-353) give the gas
     // concentrations c_k = p x_k / (R T) = u_k / M_k exactly; p = R T sum_k c_k
@@ -455,7 +481,7 @@ __device__ __forceinline__ void rhs(const DevMech& M, const Tab& tb_, const RVie
         third_body_sets<CPL>(M, tb, R.sp, Ctot, lane);
     }
     wave_sync();
-    production<CPL>(M, tb, R, R_GAS * T, lane);                  // :344, :355
+    production<CPL>(M, tb, R, R_GAS * T, lane, kp);              // :344, :355
     wave_sync();
     double w[CPL], sf[CPL];
 #pragma unroll
@@ -492,7 +518,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
     BR_GLOBAL double* Jsave = launder(Jsave_);
     BR_GLOBAL double* jscr = launder(jscr_);
     const Tab tb = tab_view<CPL>(br_lds, M);
-    const RView R = rview<CPL>((char*)R_.sp, M);
+    const RView R = R_;
     const double RT = R_GAS * T;
     const bool xm = (MF(conv) & 2) != 0;
     double* conc = R.sp + L::CONC;
@@ -682,6 +708,29 @@ struct LUWs {
     BR_GLOBAL double* D;
 };
 
+// AGPR-resident factors (CPL = 1): after lu_factor's final gather, lane s holds row s (pivot-step
+// order) of the combined factor matrix and D^-1 in accumulation registers. They stay there
+// across the Newton iterations that reuse them, so a solve reads no memory (the global
+// workspace copy is never written). Every def and use is an inline-asm operand with the "a"
+// constraint, so the register allocator keeps the values in AGPRs (2 x 32-bit per double);
+// all indices are compile-time (unrolled loops), so no dynamic register indexing.
+template <int NMAX>
+struct AccFac {
+    unsigned lo[NMAX], hi[NMAX];
+    unsigned dlo, dhi;
+};
+__device__ __forceinline__ void acc_put(unsigned& alo, unsigned& ahi, double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    asm("v_accvgpr_write_b32 %0, %1" : "=a"(alo) : "v"((unsigned)b));
+    asm("v_accvgpr_write_b32 %0, %1" : "=a"(ahi) : "v"((unsigned)(b >> 32)));
+}
+__device__ __forceinline__ double acc_get(unsigned alo, unsigned ahi) {
+    unsigned lo, hi;
+    asm("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(alo));
+    asm("v_accvgpr_read_b32 %0, %1" : "=v"(hi) : "a"(ahi));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
 // entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane =
 // original row), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
@@ -739,9 +788,9 @@ __device__ __forceinline__ double lane_pull(double v, int src) {
 // is factored right-looking. The arithmetic is exactly that of the unblocked right-looking LU.
 // Finally the rows of M are permuted into step order in place (gather, then store), and D^-1
 // is stored in step order. Returns 0 or k+1 for a zero pivot; *perm_out = pivot_perm.
-template <int NMAX>
+template <int NMAX, bool ACC = false>
 __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
-                                         int lane, int& perm_out) {
+                                         int lane, int& perm_out, AccFac<NMAX>* af = nullptr) {
     constexpr int P = NMAX < 32 ? NMAX : 32;
     constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
     constexpr int CH = 8;
@@ -810,13 +859,41 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             if (t + 1 < NC) gather(g[(t + 1) & 1], (t + 1) * CH);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * WAVE + lane] = (t * CH + i < n) ? g[t & 1][i] : 0.0;
+            for (int i = 0; i < CH; ++i) {
+                const double v = (t * CH + i < n) ? g[t & 1][i] : 0.0;
+                if constexpr (ACC) acc_put(af->lo[t * CH + i], af->hi[t * CH + i], v);
+                else F.M[(t * CH + i) * WAVE + lane] = v;
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    F.D[lane] = lane_pull(dinv, perm);
+    if constexpr (ACC) acc_put(af->dlo, af->dhi, lane_pull(dinv, perm));
+    else F.D[lane] = lane_pull(dinv, perm);
     perm_out = perm;
     return fail;
+}
+
+// solve with the AGPR-resident factors (same arithmetic and order as lu_solve): the forward
+// sweep over columns k (rows s > k), D^-1, the backward sweep (rows s < k); per column the only
+// dependency chain is readlane(r, k) -> fma, the factor reads and lane masks are off it
+template <int NMAX>
+__device__ __forceinline__ double lu_solve_acc(const AccFac<NMAX>& af, int n, int lane, int perm, double b) {
+    double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
+    const int lo = (lane < n) ? lane : -1;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) {
+        const double v = acc_get(af.lo[k], af.hi[k]);
+        const double vm = (lo > k) ? v : 0.0;
+        r = fma(-vm, bcast(r, k < n ? k : 0), r);
+    }
+    r *= acc_get(af.dlo, af.dhi);
+#pragma unroll
+    for (int k = NMAX - 1; k >= 0; --k) {
+        const double v = acc_get(af.lo[k], af.hi[k]);
+        const double vm = (lane < ((k < n) ? k : 0)) ? v : 0.0;
+        r = fma(-vm, bcast(r, k < n ? k : 0), r);
+    }
+    return (lane < n) ? r : 0.0;
 }
 
 // one triangular sweep over step-ordered factor columns in chunks of 8 (forward: k ascending,
