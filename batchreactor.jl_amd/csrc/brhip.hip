@@ -863,17 +863,28 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
 // n <= 64 keeps 256-thread workgroups (2 x 4 or 4 x 2 reactors, 8 waves/CU, VGPR-limited)
-__host__ __device__ constexpr int br_maxrpb(int nmax) { return nmax > 64 ? 8 : 4; }
+#ifndef BR_MAXRPB56
+#define BR_MAXRPB56 16   // n in 33..64: one workgroup of up to 16 reactors per CU (tables staged once)
+#endif
+#ifndef BR_MAXRPB72
+#define BR_MAXRPB72 8   // n > 64 (gas + surface): one workgroup of up to 8 reactors per CU (tables staged once)
+#endif
+__host__ __device__ constexpr int br_maxrpb(int nmax) {
+    return nmax > 64 ? BR_MAXRPB72 : (nmax == 56 || nmax == 64) ? BR_MAXRPB56 : 4;
+}
 constexpr size_t LDS_PER_CU = 160 * 1024, LDS_GRANULE = 1280;   // gfx950 (granule: conservative)
 #ifndef BR_WPE32
 #define BR_WPE32 3   // n <= 32 (surface-only): 3 waves/SIMD, 12 waves/CU (LDS allows it; 130k -> 156k/s)
 #endif
 // minimum waves per SIMD the register allocator must allow, per instance
+#ifndef BR_WPE72
+#define BR_WPE72 2   // n > 64: 2 waves/SIMD
+#endif
 #ifndef BR_WPE56
-#define BR_WPE56 3   // n in 33..64 (GRI): 3 waves/SIMD (<= 168 VGPRs; LDS allows 12 reactors/CU)
+#define BR_WPE56 4   // n in 33..64 (GRI): 4 waves/SIMD (<= 128 VGPRs; 16 x 8.8 KB + tables fit the LDS)
 #endif
 __host__ __device__ constexpr int br_wpe(int nmax) {
-    return nmax == 32 ? BR_WPE32 : (nmax == 56 || nmax == 64) ? BR_WPE56 : BR_WPE;
+    return nmax == 32 ? BR_WPE32 : (nmax == 56 || nmax == 64) ? BR_WPE56 : nmax == 72 ? BR_WPE72 : BR_WPE;
 }
 template <int NMAX>
 __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_per_eu(br_wpe(NMAX), 8))) void k_integrate(
