@@ -165,6 +165,7 @@ def main():
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                 "traffic_unit": "B per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, per reactor x N)",
                 "traffic_source": traffic_src, "kernel": eng.kernel_name, "kernel_ms": kernel_ms,
+                "launch": eng.launch_info,
                 "algorithmic_flop_per_launch": flops,
                 "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
                         "algorithmic_GBs": alg_bytes / kernel_s / 1e9,
