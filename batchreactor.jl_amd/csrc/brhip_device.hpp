@@ -577,6 +577,60 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
     }
     __builtin_amdgcn_s_waitcnt(0);   // scratch stores complete before other lanes read them
     wave_sync();
+    if (CPL == 1 && MF(nrs) == 0) {
+        // gas-only: three columns per pass (accumulators accw | accs | mc: the surface sums and the
+        // third-body sums are idle here), over the concatenated column lists of j0..j0+2 (contiguous
+        // in col_rx), so 18 passes with 3 wave barriers each instead of 53 for GRI
+        double* mcb = R.sp + L::MC;
+        const int n = MF(n);
+#pragma unroll 1
+        for (int j0 = 0; j0 < n; j0 += 3) {
+            if (lane < n) { accw[lane] = 0.0; accs[lane] = 0.0; mcb[lane] = 0.0; }
+            wave_sync();
+            const int* cp = MF(col_ptr);
+            const int cb = cp[j0], c1 = cp[min(j0 + 1, n)], c2 = cp[min(j0 + 2, n)], ce = cp[min(j0 + 3, n)];
+#pragma unroll 1
+            for (int i = cb + lane; i < ce; i += WAVE) {
+                const int r = MF(col_rx)[i];
+                const int j = j0 + (i >= c1) + (i >= c2);
+                double* acc = (i >= c2) ? mcb : (i >= c1) ? accs : accw;
+                const uint32_t* rec = tb.rx + RX_WORDS * r;
+                const uint32_t info = rec[2];
+                const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
+                const double pre = ld_l2(jscr + 2 * r);
+                double d = 0.0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) if (e < nf && sp8(rec[0], e) == j) {
+                    double pr = R.rxd[2 * r];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nf) pr *= conc[sp8(rec[0], e2)];
+                    d += pre * pr;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) if (e < nr && sp8(rec[1], e) == j) {
+                    double pr = R.rxd[2 * r + 1];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= conc[sp8(rec[1], e2)];
+                    d -= pre * pr;
+                }
+                if (tbk && j < MF(ng)) d += ld_l2(jscr + 2 * r + 1) * MF(tb_eff)[gi_tbidx(info) * n + j];
+                scatter(acc, rec[4], rec[5], rec[6], d);
+            }
+            wave_sync();
+            const double Mk = tb.molwt[lane];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int j = j0 + c;
+                if (j < n) {
+                    const double* acc = c == 0 ? accw : c == 1 ? accs : mcb;
+                    const double w = lane < n ? acc[lane] : 0.0;
+                    Jsave[j * JW + lane] = (lane < n) ? Mk * w / tb.molwt[j] : 0.0;
+                }
+            }
+            wave_sync();
+        }
+        return;
+    }
 #pragma unroll 1
     for (int j = 0; j < MF(n); ++j) {
 #pragma unroll
