@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     // BR_ACC_NMAX); otherwise in the per-slot global workspace
     constexpr bool ACCF = (CPL == 1) && (NMAX <= BR_ACC_NMAX);
     AccFac<ACCF ? NMAX : 1> af;
-    LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // LU scratch (CPL = 2): the production sums are idle then
+    LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // LU scratch (pivot-row buffer): the production sums are idle then
     double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
     for (;;) {
         double y[CPL], f[CPL];
@@ -1029,8 +1029,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            if constexpr (ACCF) lu_fail = lu_factor<NMAX, true>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], &af);
-            else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
+            if constexpr (ACCF) lu_fail = lu_factor<NMAX, true>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], scr, &af);
+            else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], scr);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
         }
@@ -1860,13 +1860,14 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     const int rid = blockIdx.x;
     if (rid >= N) return;
     const int lane = threadIdx.x;
+    __shared__ double prow[64];
     double* Jt = ws + (size_t)rid * (NMAX * WAVE + lu_ws_doubles(NMAX));
     double* LU = Jt + NMAX * WAVE;
     for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     int perm = lane;
-    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm, (LDSd*)prow);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0);

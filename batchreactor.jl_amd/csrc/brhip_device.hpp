@@ -761,6 +761,27 @@ struct LUWs {
     BR_GLOBAL double* M;
     BR_GLOBAL double* D;
 };
+typedef __attribute__((address_space(3))) double LDSd;
+typedef __attribute__((address_space(3))) int LDSi;
+
+// Pivot-row broadcast through LDS (BR_LU_LDSB = 1, off by default): per elimination step the pivot lane writes its
+// live row segment to a 64-double LDS row buffer (ds_write_b128 from one lane) and every lane reads
+// it back as broadcast ds_read_b128, so the rank-1 update costs one VALU FMA per element instead of
+// two v_readlane_b32 + FMA (at 4 waves/SIMD the integrator is VALU-issue-bound).
+#ifndef BR_LU_LDSB
+#define BR_LU_LDSB 0   // measured: GRI 75.8k vs 85.2k, surf 156k vs 174k reactors/s (the LDS round trip sits on the elimination chain)
+#endif
+template <int W>
+__device__ __forceinline__ void prow_put(LDSd* pr, const double (&a)[W], int off, int live) {
+    // pr[j] = a[j + off] for the chunks j < live (off = 1: the shifted right-looking segment)
+#pragma unroll
+    for (int c = 0; c < W; c += 8) {
+        if (c < live) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pr[c + i] = (c + i + off < W) ? a[c + i + off] : 0.0;
+        }
+    }
+}
 
 // AGPR-resident factors (CPL = 1): after lu_factor's final gather, lane s holds row s (pivot-step
 // order) of the combined factor matrix and D^-1 in accumulation registers. They stay there
@@ -793,7 +814,7 @@ __device__ __forceinline__ double acc_get(unsigned alo, unsigned ahi) {
 #endif
 template <int W>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
-                                            double& dinv, int& fail, const LUWs& F) {
+                                            double& dinv, int& fail, const LUWs& F, LDSd* pr) {
     constexpr int CH = BR_LU_CH;   // live-column granularity of the rank-1 update
     static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
@@ -808,17 +829,28 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
         F.M[k * WAVE + lane] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
         if (isp) { pstep = k; dinv = rinv; }
         const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
+#if BR_LU_LDSB
+        if (isp) prow_put<W>(pr, a, 1, live);
+        wave_sync();
+#endif
 #pragma unroll
         for (int c = 0; c < W; c += CH) {
             if (c < live) {
 #pragma unroll
                 for (int i = 0; i < CH; ++i) {
                     const int j = c + i;
+#if BR_LU_LDSB
+                    if (j + 1 < W) a[j] = fma(-(double)pr[j], l, a[j + 1]);
+#else
                     if (j + 1 < W) a[j] = fma(-bcast(a[j + 1], p), l, a[j + 1]);
+#endif
                     else a[j] = 0.0;
                 }
             }
         }
+#if BR_LU_LDSB
+        wave_sync();
+#endif
     }
 }
 
@@ -844,7 +876,7 @@ __device__ __forceinline__ double lane_pull(double v, int src) {
 // is stored in step order. Returns 0 or k+1 for a zero pivot; *perm_out = pivot_perm.
 template <int NMAX, bool ACC = false>
 __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
-                                         int lane, int& perm_out, AccFac<NMAX>* af = nullptr) {
+                                         int lane, int& perm_out, LDSd* pr, AccFac<NMAX>* af = nullptr) {
     constexpr int P = NMAX < 32 ? NMAX : 32;
     constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
     constexpr int CH = 8;
@@ -864,7 +896,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (j < n && act) ? J[j * WAVE + lane] : 0.0;
             a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
         }
-        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F);
+        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F, pr);
     }
     if (NMAX > P && n > P) {
         double b[W2];
@@ -886,16 +918,25 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #pragma unroll
             for (int i = 0; i < CH; ++i) {
                 const int k = kb + i;
+#if BR_LU_LDSB
+                if (pstep == k) prow_put<W2>(pr, b, 0, W2);
+                wave_sync();
+                const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
+#pragma unroll
+                for (int j = 0; j < W2; ++j) b[j] = fma(-(double)pr[j], l, b[j]);
+                wave_sync();
+#else
                 const unsigned long long m = __ballot(pstep == k);
                 const int p = (int)__builtin_ctzll(m);
                 const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
 #pragma unroll
                 for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), l, b[j]);
+#endif
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
         }
-        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F);
+        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F, pr);
     }
     // rows into step order, in place: chunk c is gathered completely before it is stored, and
     // the gathers of chunk c+1 are in flight while chunk c is stored (columns >= n: zeros)
@@ -956,6 +997,35 @@ __device__ __forceinline__ double lu_solve_acc(const AccFac<NMAX>& af, int n, in
 // rows a chunk cannot touch re-read a row it does touch (same 128-B lines, no extra traffic)
 // and columns past n re-read column n-1; the per-column lane masks discard what they feed.
 // Two register buffers alternate: each chunk's loads are issued a full chunk ahead of use.
+#ifndef BR_TRI_DIAG
+#define BR_TRI_DIAG 1   // masked-out lanes load the (zero) diagonal entry instead of being masked
+#endif
+// Diagonal-redirect form (BR_TRI_DIAG): the step-ordered factor matrix holds an exact 0 at (k, k)
+// and in every row >= n, so a lane that must not update in column k loads row k of that column:
+// row = max(lane, k) in the forward sweep (rows > k update), min(lane, k) in the backward sweep
+// (rows < k). The loaded factor is then the masked one, with no compare/select per column, and
+// row k shares a 128-B line with the rows that do update except at 3 line boundaries.
+template <bool FWD>
+__device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned lane8) {
+    // raw buffer loads: per-lane offset max/min(lane, k) * 8 in the VGPR, the chunk's column base
+    // c * 512 B in soffset and the column within the chunk as the immediate (<= 3584 B): one VALU
+    // op per column and no per-column 64-bit address arithmetic
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const unsigned k8 = (unsigned)(c + i) * 8u;
+        const unsigned off = FWD ? max(lane8, k8) : min(lane8, k8);
+        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (WAVE * 8), c * (WAVE * 8), 0));
+    }
+}
+template <bool FWD>
+__device__ __forceinline__ void tri_chunk_diag(const double (&v)[8], int c, int n, double& r) {
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+        const int i = FWD ? ii : 7 - ii;
+        const int k = c + i;
+        r = fma(-v[i], bcast(r, k < n ? k : 0), r);
+    }
+}
 template <bool FWD>
 __device__ __forceinline__ void tri_chunk(const double (&v)[8], int c, int lo, int n, double& r) {
     // the lane masks zero the factor entries up front (off the r dependency chain): a lane that
@@ -1020,9 +1090,17 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
     // flight while the forward sweep finishes (the factors come from L2 / Infinity Cache)
     constexpr int NCH = NMAX / 8, NT = 2 * NCH, DB = BR_TRI_DEPTH;
     double A[DB][8];
+    const unsigned lane8 = (unsigned)lane * 8u;
+    // buffer descriptor over the factor matrix (gfx9 dword 3; records = its byte size)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, NMAX * WAVE * 8, 0x00020000);
     auto load = [&](int t) {
+#if BR_TRI_DIAG
+        if (t < NCH) tri_load_diag<true>(A[t % DB], rs, t * 8, lane8);
+        else tri_load_diag<false>(A[t % DB], rs, (NT - 1 - t) * 8, lane8);
+#else
         if (t < NCH) tri_load<true>(A[t % DB], wsg, t * 8, lane, n);
         else tri_load<false>(A[t % DB], wsg, (NT - 1 - t) * 8, lane, n);
+#endif
     };
     const double dinv = wsg[NMAX * WAVE + lane];   // D^-1
     double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
@@ -1034,8 +1112,13 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
         __builtin_amdgcn_sched_barrier(0);
         if (t + DB - 1 < NT) load(t + DB - 1);
         __builtin_amdgcn_sched_barrier(0);
+#if BR_TRI_DIAG
+        if (t < NCH) tri_chunk_diag<true>(A[t % DB], t * 8, n, r);
+        else tri_chunk_diag<false>(A[t % DB], (NT - 1 - t) * 8, n, r);
+#else
         if (t < NCH) tri_chunk<true>(A[t % DB], t * 8, lo, n, r);
         else tri_chunk<false>(A[t % DB], (NT - 1 - t) * 8, lane, n, r);
+#endif
         if (t == NCH - 1) r *= dinv;
     }
     return (lane < n) ? r : 0.0;
@@ -1047,8 +1130,6 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
 // panels are 16 columns wide (registers: 2 x 16 per lane); the inverse permutation and the
 // row gathers of P b and D^-1 go through LDS scratch (>= 192 doubles) instead of ds_permute.
 // ------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) double LDSd;
-typedef __attribute__((address_space(3))) int LDSi;
 
 __device__ __forceinline__ int pivot_row2(double v0, bool c0, double v1, bool c1) {
     const unsigned long long b0 = (unsigned long long)__double_as_longlong(v0);
