@@ -1023,7 +1023,7 @@ __device__ __forceinline__ void tri_chunk_diag(const double (&v)[8], int c, int 
     for (int ii = 0; ii < 8; ++ii) {
         const int i = FWD ? ii : 7 - ii;
         const int k = c + i;
-        r = fma(-v[i], bcast(r, k < n ? k : 0), r);
+        r = fma(-v[i], bcast(r, k), r);   // k >= n: a padding column of zeros, x finite
     }
 }
 template <bool FWD>
@@ -1309,6 +1309,48 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
 // forward / backward sweeps over the step-ordered 128-row columns (fully unrolled: the column
 // of every FMA, and so the lane and row set holding r[k], are compile-time constants)
 template <bool FWD, int NMAX>
+__device__ __forceinline__ void tri_sweep2_diag(const BR_GLOBAL double* __restrict__ col, int lane, int n,
+                                                double (&r)[2]) {
+    // diagonal-redirect loads (see tri_load_diag): the step-ordered factor matrix is 0 at (k, k)
+    // and in every row >= n; first-half rows use max/min(row, k); second-half rows that cannot
+    // update are sent to k (backward) or, in the forward sweep, clamped into the 128-B line of
+    // rows 64..79, whose rows >= n (n <= 72) are zero -- so no extra lines and no selects
+    constexpr int JW = 128, NCH = NMAX / 8;
+    static_assert(NMAX <= 72, "rows n..79 must be padding");
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)col, (short)0, NMAX * JW * 8, 0x00020000);
+    const unsigned lane8 = (unsigned)lane * 8u, hi8 = lane8 + 512u;
+    double v[2][2][8];
+    auto load = [&](double (&b)[2][8], int c) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const unsigned k8 = (unsigned)(c + i) * 8u;
+            const unsigned o0 = FWD ? max(lane8, k8) : min(lane8, k8);
+            const unsigned o1 = FWD ? min(max(hi8, k8), 79u * 8u) : min(hi8, k8);
+            const int cb = (c + i) * JW * 8;
+            b[0][i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, 0));
+            b[1][i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, cb, 0));
+        }
+    };
+    auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
+    load(v[0], cidx(0));
+    if (NCH > 1) load(v[1], cidx(1));
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int c = cidx(t);
+#pragma unroll
+        for (int ii = 0; ii < 8; ++ii) {
+            const int i = FWD ? ii : 7 - ii;
+            const int k = c + i;
+            const double x = bcast(r[k >> 6], k & 63);   // padding columns: x finite, factors 0
+#pragma unroll
+            for (int s = 0; s < 2; ++s) r[s] = fma(-v[t & 1][s][i], x, r[s]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < NCH) load(v[t & 1], cidx(t + 2));
+    }
+}
+template <bool FWD, int NMAX>
 __device__ __forceinline__ void tri_sweep2(const BR_GLOBAL double* __restrict__ col, int lane, int n, double (&r)[2]) {
     constexpr int JW = 128, NCH = NMAX / 8;
     double v[2][2][8];
@@ -1363,10 +1405,18 @@ __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* s
     wave_sync();
     double r[2] = {dsc[perm[0]], dsc[perm[1]]};   // P b
     wave_sync();
+#if BR_TRI_DIAG
+    tri_sweep2_diag<true, NMAX>(wsg, lane, n, r);
+#else
     tri_sweep2<true, NMAX>(wsg, lane, n, r);
+#endif
     r[0] *= wsg[NMAX * JW + lane];
     r[1] *= wsg[NMAX * JW + 64 + lane];
+#if BR_TRI_DIAG
+    tri_sweep2_diag<false, NMAX>(wsg, lane, n, r);
+#else
     tri_sweep2<false, NMAX>(wsg, lane, n, r);
+#endif
     b[0] = (lane < n) ? r[0] : 0.0;
     b[1] = (lane + 64 < n) ? r[1] : 0.0;
 }
