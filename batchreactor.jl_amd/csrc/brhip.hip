@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         if (!lu_fail) {
             BR_CLK(c0);
             if constexpr (ACCF) delta[0] = lu_solve_acc<NMAX>(af, n, lane, perm[0], b[0]);
-            else if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0]);
+            else if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
             else {
                 lu_solve2<NMAX>(LUsave, scr, n, lane, perm, b);
                 delta[0] = b[0];
@@ -1870,7 +1870,7 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm, (LDSd*)prow);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
-    const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0);
+    const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0, (LDSd*)prow);
     if (lane < n) x[(size_t)rid * n + lane] = r;
     if (lane == 0) fail[rid] = f;
 }

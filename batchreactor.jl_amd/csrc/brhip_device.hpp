@@ -151,6 +151,18 @@ __device__ __forceinline__ double bcast_x(double v, int lane_addr4) {
     const int hi = __builtin_amdgcn_ds_bpermute(lane_addr4, (int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// broadcast of a pivot-row element in the LU: through the LDS crossbar (BR_LU_XBAR = 1: two
+// ds_bpermute on the LDS pipe, no VALU issue; the kernel is VALU-issue-bound) or v_readlane
+#ifndef BR_LU_XBAR
+#define BR_LU_XBAR 0   // measured: GRI 78.2k vs 90.8k, gas+surf 16.8k vs 17.8k reactors/s (the bpermute latency sits on the elimination chain)
+#endif
+__device__ __forceinline__ double bcast_lu(double v, int p) {
+#if BR_LU_XBAR
+    return bcast_x(v, p * 4);
+#else
+    return bcast(v, p);
+#endif
+}
 __device__ __forceinline__ double uni(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
@@ -842,7 +854,7 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
 #if BR_LU_LDSB
                     if (j + 1 < W) a[j] = fma(-(double)pr[j], l, a[j + 1]);
 #else
-                    if (j + 1 < W) a[j] = fma(-bcast(a[j + 1], p), l, a[j + 1]);
+                    if (j + 1 < W) a[j] = fma(-bcast_lu(a[j + 1], p), l, a[j + 1]);
 #endif
                     else a[j] = 0.0;
                 }
@@ -930,7 +942,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
                 const int p = (int)__builtin_ctzll(m);
                 const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
 #pragma unroll
-                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast(b[j], p), l, b[j]);
+                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast_lu(b[j], p), l, b[j]);
 #endif
             }
 #pragma unroll
@@ -1078,13 +1090,111 @@ __device__ __forceinline__ double tri_sweep(const BR_GLOBAL double* __restrict__
     return r;
 }
 
+// ---- DPP form of the triangular sweeps (BR_TRI_DPP): the columns go in blocks of 16, one block
+// per 16-lane DPP row. Block b first runs its diagonal 16 x 16 part inside row b: r += -M[s][k] *
+// r[k], with r[k] broadcast from lane k of the row by the DPP modifier of the FMA itself
+// (v_fmac_f64 row_newbcast) and the write limited to row b by the DPP row mask: one VALU op per
+// column instead of two v_readlane + FMA, no exec change, no branch. The finished values of row
+// b are then copied to every row through LDS (one write, one read) and the rows below (forward)
+// / above (backward) apply the block's columns with the same DPP FMA on the copy. Every lane
+// still accumulates its columns in the same order with the same fma(-M[s][k], r[k], r[s]), so
+// the result is bit-identical to tri_chunk_diag's.
+#ifndef BR_TRI_DPP
+#define BR_TRI_DPP 1
+#endif
+// r += -f * r[row base + K] in the rows of RM; the s_nop covers the VALU-write -> DPP-read
+// hazard on r (the previous op of the chain wrote it)
+template <int K, int RM>
+__device__ __forceinline__ void dpp_fnma_self(double& r, double f) {
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, -%1 row_newbcast:%2 row_mask:%3 bank_mask:0xf"
+                 : "+v"(r) : "v"(f), "i"(K), "i"(RM));
+}
+// r += -f * x[row base + K] in the rows of RM
+template <int K, int RM>
+__device__ __forceinline__ void dpp_fnma(double& r, double x, double f) {
+    asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:%4 bank_mask:0xf"
+                 : "+v"(r) : "v"(x), "v"(f), "i"(K), "i"(RM));
+}
+template <bool FWD, int CW, int RM, int I>
+__device__ __forceinline__ void dpp_diag(double& r, const double (&v)[16]) {
+    if constexpr (I < CW) {
+        constexpr int K = FWD ? I : CW - 1 - I;
+        dpp_fnma_self<K, RM>(r, v[K]);
+        dpp_diag<FWD, CW, RM, I + 1>(r, v);
+    }
+}
+template <bool FWD, int CW, int RM, int I>
+__device__ __forceinline__ void dpp_off(double& r, double x, const double (&v)[16]) {
+    if constexpr (I < CW) {
+        constexpr int K = FWD ? I : CW - 1 - I;
+        dpp_fnma<K, RM>(r, x, v[K]);
+        dpp_off<FWD, CW, RM, I + 1>(r, x, v);
+    }
+}
+// block T of a sweep (blocks of 16 columns, the last one NMAX % 16 wide if that is not 0),
+// factor loads one block ahead (diagonal-redirect offsets, see tri_load_diag); x64 = 64 doubles
+// of LDS scratch
+template <bool FWD, int NMAX, int T>
+__device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigned lane8, double& r, LDSd* x64,
+                                              double (&v)[2][16]) {
+    constexpr int NB = (NMAX + 15) / 16;
+    if constexpr (T < NB) {
+        constexpr int B = FWD ? T : NB - 1 - T;            // block = DPP row
+        constexpr int CW = (16 * B + 16 > NMAX) ? NMAX - 16 * B : 16;
+        auto load = [&](double (&d)[16], int blk) {
+            tri_load_diag<FWD>(*reinterpret_cast<double(*)[8]>(&d[0]), rs, 16 * blk, lane8);
+            if (16 * blk + 8 < NMAX) tri_load_diag<FWD>(*reinterpret_cast<double(*)[8]>(&d[8]), rs, 16 * blk + 8, lane8);
+        };
+        if constexpr (T == 0) load(v[0], B);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (T + 1 < NB) load(v[(T + 1) & 1], FWD ? B + 1 : B - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const double (&f)[16] = v[T & 1];
+        dpp_diag<FWD, CW, 1 << B, 0>(r, f);
+        constexpr int ROWS = FWD ? (0xF << (B + 1)) & 0xF : (1 << B) - 1;   // rows still to update
+        if constexpr (ROWS != 0) {
+            asm volatile("s_nop 1");                       // r: DPP-encoded VALU write (inline asm)
+            x64[(lane8 >> 3)] = r;
+            wave_sync();
+            const double x = x64[16 * B + ((lane8 >> 3) & 15)];
+            dpp_off<FWD, CW, ROWS, 0>(r, x, f);
+            wave_sync();
+        }
+        tri_block_dpp<FWD, NMAX, T + 1>(rs, lane8, r, x64, v);
+    }
+}
+template <bool FWD, int NMAX>
+__device__ __forceinline__ void tri_sweep_dpp(__amdgpu_buffer_rsrc_t rs, int lane, double& r, LDSd* x64) {
+    double v[2][16];
+    tri_block_dpp<FWD, NMAX, 0>(rs, (unsigned)lane * 8u, r, x64, v);
+    asm volatile("s_nop 1");
+}
+
 // solve (I - gamma J) x = b with the factors of lu_factor: L y = P b, y' = D^-1 y, U' x = y'.
 // `perm` from lu_factor; b and the returned x are in natural component order (the backward
 // sweep leaves unknown s, i.e. column s, on lane s).
 template <int NMAX>
-__device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n, int lane, int perm, double b) {
+__device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n, int lane, int perm, double b,
+                                           LDSd* x16) {
     const BR_GLOBAL double* wsg = launder(ws);
     lane = launder_v(lane);
+#if BR_TRI_DPP
+    if constexpr (NMAX % 8 == 0) {
+        // one buffer descriptor over factors + D^-1: every load of the solve is a buffer load, so
+        // the waitcnt pass can count them in order (a global load among them forces vmcnt(0))
+        // (and nothing issued before the solve may still be pending: a flat or scratch access of the
+        // controller would make the counter out of order too -- so drain it first)
+        __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0)
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * WAVE * 8, 0x00020000);
+        const double dinv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * WAVE * 8, 0));
+        double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
+        tri_sweep_dpp<true, NMAX>(rs, lane, r, x16);
+        r *= dinv;
+        tri_sweep_dpp<false, NMAX>(rs, lane, r, x16);   // (x16: 64 doubles of LDS scratch)
+        return (lane < n) ? r : 0.0;
+    }
+#endif
     // the forward (unit lower) and backward (unit upper) sweeps run as ONE chunk sequence with
     // one prefetch pipeline, so the backward sweep's first columns and D^-1 are already in
     // flight while the forward sweep finishes (the factors come from L2 / Infinity Cache)
@@ -1178,7 +1288,7 @@ __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, 
                     for (int i = 0; i < CH; ++i) {
                         const int j = c + i;
                         if (j + 1 < W) {
-                            const double u = bcast(a[src][j + 1], p);
+                            const double u = bcast_lu(a[src][j + 1], p);
                             a[0][j] = fma(-u, l[0], a[0][j + 1]);
                             a[1][j] = fma(-u, l[1], a[1][j + 1]);
                         } else {
@@ -1230,7 +1340,7 @@ __device__ __forceinline__ void lu2_panels(const BR_GLOBAL double* J, double gam
                         constexpr int src = decltype(S)::value;
 #pragma unroll
                         for (int j = 0; j < W; ++j) {
-                            const double u = bcast(a[src][j], p);
+                            const double u = bcast_lu(a[src][j], p);
                             a[0][j] = fma(-u, l0, a[0][j]);
                             a[1][j] = fma(-u, l1, a[1][j]);
                         }
