@@ -9,7 +9,7 @@
 //      SX records (48 B / surface reaction) | SXE (4 doubles / surface reaction: coverage eps) |
 //      TBE third-body entries (16 B: species, eff-1)
 //  * per reactor block: [Ctl][V: Nordsieck + work vectors][SP: conc | accw | accs (64 each)]
-//      [FOD: {k0, log10 Fcent, c, n} per falloff reaction][SKD: {k, k*exp(cov)} per surface reaction]
+//      [FOD: {k0/k_inf, log10 Fcent, c, n} per falloff reaction][SKD: {k, k*exp(cov)} per surface reaction]
 //  * RXD: {kf, kr} per gas reaction, in the wave's global workspace slot (5.2 KB for GRI: kept
 //    out of LDS so 12 reactors fit a CU instead of 8), prefetched at the start of each RHS
 //  * T-dependent rate constants (RXD/FOD/SKD) are computed once per reactor: T is a per-reactor
@@ -211,7 +211,7 @@ __device__ __forceinline__ int launder_v(int v) {
 struct RView {
     double* sp;    // species block: conc[k] = sp[CONC+k], accw, accs, mc (see Lay)
     BR_GLOBAL double* rxd;   // kf = rxd[2r], kr = rxd[2r+1] (global workspace slot)
-    double* fod;   // k0, log10 Fcent, c, n per falloff reaction
+    double* fod;   // k0/k_inf, log10 Fcent, c, n per falloff reaction
     double* skd;   // k(T), k*exp(-sum eps theta/RT) (Jacobian) per surface reaction
 };
 __host__ __device__ inline int fod_off_bytes(int /*nrg*/) { return 0; }   // RXD is in global memory
@@ -292,7 +292,7 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
             const int fi = gi_foidx(info);
             const double* fp = MF(fo_par) + 8 * fi;
             double* fo = R.fod + 4 * fi;
-            fo[0] = fp[0] * exp(fp[1] * lT - fp[2] / T);
+            fo[0] = fp[0] * exp(fp[1] * lT - fp[2] / T) / kf;   // k0 / k_inf
             double fcv = 1.0;
             if (gi_troe(info)) {
                 fcv = (1 - fp[3]) * exp(-T / fp[4]) + fp[3] * exp(-T / fp[5]);
@@ -320,29 +320,35 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
     wave_sync();
 }
 
-// falloff: fac = Pr/(1+Pr)*F and d fac / d[M] (CHEMKIN Lindemann / Troe)
+// falloff: fac = Pr/(1+Pr)*F and d fac / d[M] (CHEMKIN Lindemann / Troe); fo[0] = k0/k_inf
+// (T-only, so Pr = fo[0] [M] needs no division). Troe: log10 F = log10 Fcent / (1 + f1^2) with
+// f1 = x / den, evaluated as log10 Fcent den^2 / (den^2 + x^2) (one division), F = exp10(...)
+// instead of the generic pow(10, .) (same value to an ulp, about half the instructions).
+__device__ __forceinline__ double troe_F(double Pr, const double* fo, double& x_out, double& den_out) {
+    const double Prs = Pr > 1e-300 ? Pr : 1e-300;
+    const double x = log10(Prs) + fo[2];
+    const double den = fo[3] - 0.14 * x;
+    const double d2 = den * den;
+    x_out = x; den_out = den;
+    return exp10(fo[1] * d2 / (d2 + x * x));
+}
 template <bool WANT_D>
-__device__ __forceinline__ void falloff(const double* fo, bool troe, double kinf, double Mc, double& fac,
-                                        double& dfac) {
-    const double k0 = fo[0];
-    const double Pr = k0 * Mc / kinf;
+__device__ __forceinline__ void falloff(const double* fo, bool troe, double Mc, double& fac, double& dfac) {
+    const double k0r = fo[0];
+    const double Pr = k0r * Mc;
     double F = 1.0, g = 0.0;
     if (troe) {
-        const double Prs = Pr > 1e-300 ? Pr : 1e-300;
-        const double lfc = fo[1];
-        const double L = log10(Prs);
-        const double cc = fo[2], nn = fo[3];
-        const double den = nn - 0.14 * (L + cc);
-        const double f1 = (L + cc) / den;
-        const double lF = lfc / (1 + f1 * f1);
-        F = pow(10.0, lF);
+        double x, den;
+        F = troe_F(Pr, fo, x, den);
         if (WANT_D) {
+            const double lfc = fo[1], nn = fo[3];
+            const double f1 = x / den;
             const double df1 = nn / (den * den);
             g = -lfc * 2 * f1 / ((1 + f1 * f1) * (1 + f1 * f1)) * df1;
         }
     }
     fac = Pr / (1 + Pr) * F;
-    if (WANT_D) dfac = (F / ((1 + Pr) * (1 + Pr)) + F * g / (1 + Pr)) * (k0 / kinf);
+    if (WANT_D) dfac = (F / ((1 + Pr) * (1 + Pr)) + F * g / (1 + Pr)) * k0r;
 }
 
 // third-body concentrations of the efficiency sets: mc[s] = Ctot + sum (eff-1) c over the set's
@@ -415,7 +421,7 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
             if (tbk == 1) D *= Mc;
             else {
                 double fac, dfac;
-                falloff<false>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, k.x, Mc, fac, dfac);
+                falloff<false>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
                 D *= fac;
                 if (xm) D *= Mc * 1e-6;                                // [M] in mol/cm3
             }
@@ -567,7 +573,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
             if (tbk == 1) { pre = Mc; coefM = 1.0; }
             else {
                 double fac, dfac;
-                falloff<true>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, kf, Mc, fac, dfac);
+                falloff<true>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
                 pre = fac * (xm ? Mc * 1e-6 : 1.0);
                 coefM = dfac * (xm ? Mc * 1e-6 : 1.0) + (xm ? fac * 1e-6 : 0.0);
             }
@@ -866,6 +872,81 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
     }
 }
 
+// ---- pivot rows through LDS, one step ahead (BR_LU_LA) ----------------------------------
+// The rank-1 update needs the pivot row a_p[k+1..] in every lane. Broadcasting it element by
+// element costs two v_readlane + the FMA per element (3 VALU ops, the LU's main cost); through
+// LDS it costs one FMA per element plus LDS traffic, but a write-then-read round trip per step
+// on the elimination chain was measured slower (BR_LU_LDSB). Here the round trip is taken off
+// the chain: step k updates its first chunk of 8 columns, runs the pivot search for step k+1
+// on the updated column k+1, and from then on the NEW pivot lane stores each chunk of its row
+// into the other LDS buffer as soon as step k has updated it; step k+1 reads the row from
+// there (written chunks earlier). Two buffers alternate, so a step's reads never meet the
+// next step's writes (chunk order = program order, kept by scheduling barriers; LDS executes a
+// wave's accesses in order). The arithmetic (pivot choice,
+// multipliers, FMA order) is that of lu_rl_steps.
+#ifndef BR_LU_LA
+#define BR_LU_LA 0   // measured: GRI 79.4k vs 92.4k, surf 165k vs 192k reactors/s (a broadcast LDS read moves 512 B per wave: LDS-bandwidth-bound, 2x the readlane cost per CU)
+#endif
+template <int W>
+__device__ __forceinline__ void lu_la_step(double (&a)[W], int k, int k1, int cend, int lane, int& pstep,
+                                           double& dinv, int& fail, const LUWs& F, const LDSd* ub, LDSd* nb,
+                                           int& p, double& piv) {
+    constexpr int CH = 8;
+    if (piv == 0.0 && !fail) fail = k + 1;
+    const double rinv = 1.0 / piv;
+    const bool isp = (lane == p);
+    const bool rem = (pstep < 0) && !isp;
+    const double l = rem ? a[0] * rinv : 0.0;
+    F.M[k * WAVE + lane] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
+    if (isp) { pstep = k; dinv = rinv; }
+    const int live = cend - k;                 // columns k..cend-1 are live in a[0..live-1]
+    const bool more = k + 1 < k1;
+    int pn = 0;
+    double pivn = 1.0;
+#pragma unroll
+    for (int c = 0; c < W; c += CH) {
+        __builtin_amdgcn_sched_barrier(0);     // a chunk's row reads stay with its FMAs (registers)
+        if (c < live) {
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const int j = c + i;
+                if (j + 1 < W) a[j] = fma(-(double)ub[j + 1], l, a[j + 1]);
+                else a[j] = 0.0;
+            }
+            if (more) {
+                if (c == 0) {                      // column k+1 is final for step k: next pivot
+                    pn = pivot_lane(fabs(a[0]), pstep < 0);
+                    pivn = bcast(a[0], pn);
+                }
+                if (lane == pn) {
+#pragma unroll
+                    for (int i = 0; i < CH; ++i) nb[c + i] = a[c + i];
+                }
+            }
+        }
+    }
+    p = pn;
+    piv = pivn;
+}
+// steps k0..k1-1; on entry the pivot of step k0 is not yet known (prologue: search + row store)
+template <int W>
+__device__ __forceinline__ void lu_la_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
+                                            double& dinv, int& fail, const LUWs& F, LDSd* bufA, LDSd* bufB) {
+    int p = pivot_lane(fabs(a[0]), pstep < 0);
+    double piv = bcast(a[0], p);
+    if (lane == p) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) bufA[j] = a[j];
+    }
+    LDSd* ub = bufA;
+    LDSd* nb = bufB;
+#pragma unroll 1
+    for (int k = k0; k < k1; ++k) {
+        lu_la_step<W>(a, k, k1, cend, lane, pstep, dinv, fail, F, ub, nb, p, piv);
+        LDSd* t = ub; ub = nb; nb = t;
+    }
+}
+
 // row order after factorization: lane s works on the pivot row of step s, i.e. original row
 // perm[s] (perm = inverse of pstep); lanes >= n map to themselves
 __device__ __forceinline__ int pivot_perm(int pstep, int lane, int n) {
@@ -908,7 +989,11 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (j < n && act) ? J[j * WAVE + lane] : 0.0;
             a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
         }
+#if BR_LU_LA
+        lu_la_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F, pr, pr + 64);
+#else
         lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F, pr);
+#endif
     }
     if (NMAX > P && n > P) {
         double b[W2];
@@ -918,19 +1003,47 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (col < n && act) ? J[col * WAVE + lane] : 0.0;
             b[j] = ((col == lane) ? 1.0 : 0.0) - gamma * jv;
         }
-        double cur[CH], nxt[CH];
+        // (BR_LU_LA: multipliers prefetched 4 steps ahead instead of 8; the LDS row chunk takes the
+        // registers the readlane broadcast kept in SGPRs)
+        constexpr int LL = BR_LU_LA ? 4 : CH;
+        double cur[LL], nxt[LL];
 #pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = F.M[i * WAVE + lane];
+        for (int i = 0; i < LL; ++i) cur[i] = F.M[i * WAVE + lane];
+#if BR_LU_LA
+        // pivot rows of the left-looking steps through LDS, one step ahead (see lu_la_step): the
+        // pivot lane of step k+1 (pstep == k+1) stores each chunk of its row once step k updated it
+        LDSd* const lb0 = pr;
+        LDSd* const lb1 = pr + 64;
+        if (pstep == 0) {
+#pragma unroll
+            for (int j = 0; j < W2; ++j) lb0[j] = b[j];
+        }
+#endif
 #pragma unroll 1
-        for (int kb = 0; kb < P; kb += CH) {
-            if (kb + CH < P) {
+        for (int kb = 0; kb < P; kb += LL) {
+            if (kb + LL < P) {
 #pragma unroll
-                for (int i = 0; i < CH; ++i) nxt[i] = F.M[(kb + CH + i) * WAVE + lane];
+                for (int i = 0; i < LL; ++i) nxt[i] = F.M[(kb + LL + i) * WAVE + lane];
             }
 #pragma unroll
-            for (int i = 0; i < CH; ++i) {
+            for (int i = 0; i < LL; ++i) {
                 const int k = kb + i;
-#if BR_LU_LDSB
+#if BR_LU_LA
+                const LDSd* ub = (i & 1) ? lb1 : lb0;    // static parity (kb is a multiple of LL, even)
+                LDSd* nb = (i & 1) ? lb0 : lb1;
+                const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
+                const bool nxp = (pstep == k + 1);
+#pragma unroll
+                for (int c = 0; c < W2; c += 8) {
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = c; j < c + 8 && j < W2; ++j) b[j] = fma(-(double)ub[j], l, b[j]);
+                    if (nxp) {
+#pragma unroll
+                        for (int j = c; j < c + 8 && j < W2; ++j) nb[j] = b[j];
+                    }
+                }
+#elif BR_LU_LDSB
                 if (pstep == k) prow_put<W2>(pr, b, 0, W2);
                 wave_sync();
                 const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
@@ -946,9 +1059,13 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #endif
             }
 #pragma unroll
-            for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
+            for (int i = 0; i < LL; ++i) cur[i] = nxt[i];
         }
+#if BR_LU_LA
+        lu_la_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F, pr, pr + 64);
+#else
         lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F, pr);
+#endif
     }
     // rows into step order, in place: chunk c is gathered completely before it is stored, and
     // the gathers of chunk c+1 are in flight while chunk c is stored (columns >= n: zeros)

@@ -877,7 +877,7 @@ __device__ __forceinline__ void lane_tconst(const LaneLay& LL, double* Lp, const
         if (gi_tb(info) == 2) {
             const int fi = gi_foidx(info);
             const CF64* fp = (const CF64*)MF(fo_par) + 8 * fi;
-            G.st(LL.g_fod + 4 * fi, fp[0] * exp(fp[1] * lT - fp[2] / T));
+            G.st(LL.g_fod + 4 * fi, fp[0] * exp(fp[1] * lT - fp[2] / T) / kf);   // k0 / k_inf
             double fcv = 1.0;
             if (gi_troe(info)) {
                 fcv = (1 - fp[3]) * exp(-T / fp[4]) + fp[3] * exp(-T / fp[5]);
@@ -959,17 +959,13 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
                 D *= Mc;
             } else {                                            // Lindemann / Troe falloff
                 const int fi = gi_foidx(info);
-                const double k0 = G.ld(LL.g_fod + 4 * fi);
-                const double Pr = k0 * Mc / kf;
+                const double Pr = G.ld(LL.g_fod + 4 * fi) * Mc;     // k0/k_inf [M]
                 double F = 1.0;
                 if (gi_troe(info)) {
-                    const double Prs = Pr > 1e-300 ? Pr : 1e-300;
-                    const double lfc = G.ld(LL.g_fod + 4 * fi + 1);
-                    const double L = log10(Prs);
-                    const double cc = G.ld(LL.g_fod + 4 * fi + 2), nn = G.ld(LL.g_fod + 4 * fi + 3);
-                    const double den = nn - 0.14 * (L + cc);
-                    const double f1 = (L + cc) / den;
-                    F = pow(10.0, lfc / (1 + f1 * f1));
+                    const double fo[4] = {0.0, G.ld(LL.g_fod + 4 * fi + 1), G.ld(LL.g_fod + 4 * fi + 2),
+                                          G.ld(LL.g_fod + 4 * fi + 3)};
+                    double x, den;
+                    F = troe_F(Pr, fo, x, den);
                 }
                 D *= Pr / (1 + Pr) * F;
                 if (xm) D *= Mc * 1e-6;                         // [M] in mol/cm3
@@ -1028,7 +1024,7 @@ __device__ __forceinline__ void lane_jac(const LaneLay& LL, const double* Lp, co
 #pragma unroll
                 for (int c = 0; c < 4; ++c) fo[c] = G.ld(LL.g_fod + 4 * fi + c);
                 double fac, dfac;
-                falloff<true>(fo, gi_troe(info) != 0, kf, Mc, fac, dfac);
+                falloff<true>(fo, gi_troe(info) != 0, Mc, fac, dfac);
                 const double xs = xm ? Mc * 1e-6 : 1.0;                   // [M] in mol/cm3 (reference)
                 pre = fac * xs;
                 coefM = dfac * xs + (xm ? fac * 1e-6 : 0.0);
