@@ -17,14 +17,13 @@
 #include <vector>
 
 #include "../../include/brhip.h"
-#include "brhip_device.hpp"
-
 #ifndef BR_ASM_MARKS
 #define BR_ASM_MARKS 0
 #endif
 #ifndef BR_PHASE_CLOCKS
 #define BR_PHASE_CLOCKS 0   // per-phase shader-clock counters in br_stats (diagnostic build: libbrhip_diag.so)
 #endif
+#include "brhip_device.hpp"
 
 using namespace brhip;
 
@@ -1929,3 +1928,16 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     hipFree(dJ); hipFree(dg); hipFree(db); hipFree(dx); hipFree(dws); hipFree(df);
     return 0;
 }
+
+#if BR_PHASE_CLOCKS
+// diagnostic build only (not declared in brhip.h): read and reset the sub-phase clock sums
+// (BR_SUB_ADD slots of brhip_device.hpp)
+extern "C" int br_diag_sub(double* out8) {
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(brhip::g_sub), sizeof(v)) != hipSuccess) return -1;
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(brhip::g_sub), z, sizeof(z)) != hipSuccess) return -1;
+    for (int i = 0; i < 8; ++i) out8[i] = (double)v[i];
+    return 0;
+}
+#endif

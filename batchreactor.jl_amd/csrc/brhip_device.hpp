@@ -123,6 +123,20 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
 }
 
 // ------------------------------------------------------------------------------------
+// sub-phase shader clocks (diagnostic build, BR_PHASE_CLOCKS): BR_SUB_T(t) starts a timer,
+// BR_SUB_ADD(slot, t) adds its cycles to g_sub[slot] (one atomic from lane 0); read and reset
+// from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather.
+// ------------------------------------------------------------------------------------
+#if BR_PHASE_CLOCKS
+__device__ unsigned long long g_sub[8];
+#define BR_SUB_T(t) const unsigned long long t = clock64()
+#define BR_SUB_ADD(slot, t) do { if ((threadIdx.x & 63) == 0) atomicAdd(&::brhip::g_sub[slot], clock64() - (t)); } while (0)
+#else
+#define BR_SUB_T(t)
+#define BR_SUB_ADD(slot, t)
+#endif
+
+// ------------------------------------------------------------------------------------
 // wave primitives (DPP row reductions + readlane; no LDS)
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void wave_sync() {
@@ -982,6 +996,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     double dinv = 0.0;
     int fail = 0;
     const int n1 = n < P ? n : P;
+    BR_SUB_T(lt0);
     {
         double a[P];
 #pragma unroll
@@ -995,6 +1010,8 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F, pr);
 #endif
     }
+    BR_SUB_ADD(0, lt0);
+    BR_SUB_T(lt1);
     if (NMAX > P && n > P) {
         double b[W2];
 #pragma unroll
@@ -1067,6 +1084,8 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F, pr);
 #endif
     }
+    BR_SUB_ADD(1, lt1);
+    BR_SUB_T(lt2);
     // rows into step order, in place: chunk c is gathered completely before it is stored, and
     // the gathers of chunk c+1 are in flight while chunk c is stored (columns >= n: zeros)
     const int perm = pivot_perm(pstep, lane, n);
@@ -1093,6 +1112,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     }
     if constexpr (ACC) acc_put(af->dlo, af->dhi, lane_pull(dinv, perm));
     else F.D[lane] = lane_pull(dinv, perm);
+    BR_SUB_ADD(2, lt2);
     perm_out = perm;
     return fail;
 }
