@@ -177,7 +177,16 @@ __device__ __forceinline__ double bcast_lu(double v, int p) {
     return bcast(v, p);
 #endif
 }
+// uniform fp64 values: v_readfirstlane into SGPRs (BR_UNI_D = 1) or left in VGPRs (0). fp64
+// arithmetic and compares run on the VALU either way, so the two readfirstlanes buy only SGPR
+// residency and scalar branches
+#ifndef BR_UNI_D
+#define BR_UNI_D 1
+#endif
 __device__ __forceinline__ double uni(double v) {
+#if !BR_UNI_D
+    return v;
+#endif
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
     const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));

@@ -23,7 +23,7 @@ done
 if [[ " $CFGS " == *" gri "* ]]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --no-phase > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; exit 1; }
   cp "$(ls gpurun_out/prof/*kernel_stats.csv | head -1)" gpurun_out/profiles/${TAG}_gri1e5_kernel_stats.csv
-  tail -1 gpurun_out/prof.log > gpurun_out/profiles/${TAG}_gri1e5_rocprof_bench_line.json
+  grep "^{\"metric\"" gpurun_out/prof.log | tail -1 > gpurun_out/profiles/${TAG}_gri1e5_rocprof_bench_line.json
   head -3 gpurun_out/profiles/${TAG}_gri1e5_kernel_stats.csv
 fi
 echo profile done
