@@ -1649,6 +1649,104 @@ __device__ __forceinline__ void tri_sweep2(const BR_GLOBAL double* __restrict__ 
     }
 }
 
+// DPP form of the CPL = 2 sweeps (BR_TRI_DPP; 64 < n <= NMAX = 72): r0 holds row lane, r1 row lane + 64
+// (lanes 0..NMAX-65 real, the rest of DPP row 0 is zero padding). Column blocks 0..3 are rows 0..63 in r0
+// (DPP row b), block 4 = columns 64..NMAX-1 is DPP row 0 of r1. Forward: block b's diagonal part in
+// row b of r0, its finished values copied to every row through LDS, then the rows of r0 below it and
+// the r1 rows (all below) apply it; block 4 last, inside r1. Backward: block 4 first inside r1, its
+// values applied to every r0 row, then blocks 3..0 in r0 (r1 rows are below them: untouched). Same
+// per-lane FMA order as tri_sweep2_diag, so bit-identical.
+template <bool FWD, int CW>
+__device__ __forceinline__ void tri2_load_blk(double (&v0)[16], double (&v1)[16], __amdgpu_buffer_rsrc_t rs, int c0,
+                                              unsigned lane8, unsigned hi8, bool want0, bool want1) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i < CW) {
+            const unsigned k8 = (unsigned)(c0 + i) * 8u;
+            const int cb = (c0 + i) * 128 * 8;
+            if (want0) {
+                const unsigned o0 = FWD ? max(lane8, k8) : min(lane8, k8);
+                v0[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, 0));
+            }
+            if (want1) {
+                const unsigned o1 = FWD ? min(max(hi8, k8), 79u * 8u) : min(hi8, k8);
+                v1[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, cb, 0));
+            }
+        }
+    }
+}
+template <int NMAX>
+__device__ __forceinline__ void tri_sweeps2_dpp(__amdgpu_buffer_rsrc_t rs, int lane, double (&r)[2], const double (&dv)[2],
+                                                LDSd* x64) {
+    static_assert(NMAX > 64 && NMAX <= 72, "CPL = 2 DPP sweeps: 64 < NMAX <= 72");
+    constexpr int W1 = NMAX - 64;
+    const unsigned lane8 = (unsigned)lane * 8u, hi8 = lane8 + 512u;
+    const int xl = lane & 15;
+    double v[2][2][16];
+    // ---- forward: blocks 0..3 (r0), then block 4 (r1)
+    tri2_load_blk<true, 16>(v[0][0], v[0][1], rs, 0, lane8, hi8, true, true);
+    auto fwd_blk = [&](auto B_) {
+        constexpr int B = decltype(B_)::value;
+        double (&f0)[16] = v[B & 1][0];
+        double (&f1)[16] = v[B & 1][1];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (B < 3) tri2_load_blk<true, 16>(v[(B + 1) & 1][0], v[(B + 1) & 1][1], rs, 16 * (B + 1), lane8, hi8, true, true);
+        else tri2_load_blk<true, W1>(v[(B + 1) & 1][0], v[(B + 1) & 1][1], rs, 64, lane8, hi8, false, true);
+        __builtin_amdgcn_sched_barrier(0);
+        dpp_diag<true, 16, 1 << B, 0>(r[0], f0);
+        asm volatile("s_nop 1");
+        x64[lane] = r[0];
+        wave_sync();
+        const double x = x64[16 * B + xl];
+        if constexpr (B < 3) dpp_off<true, 16, (0xF << (B + 1)) & 0xF, 0>(r[0], x, f0);
+        dpp_off<true, 16, 0x1, 0>(r[1], x, f1);
+        wave_sync();
+    };
+    fwd_blk(std::integral_constant<int, 0>{});
+    fwd_blk(std::integral_constant<int, 1>{});
+    fwd_blk(std::integral_constant<int, 2>{});
+    fwd_blk(std::integral_constant<int, 3>{});
+    dpp_diag<true, W1, 0x1, 0>(r[1], v[0][1]);          // block 4 (buffer 4 & 1 = 0)
+    asm volatile("s_nop 1");
+    r[0] *= dv[0];
+    r[1] *= dv[1];
+    // ---- backward: block 4 (r1) first, then blocks 3..0 (r0)
+    tri2_load_blk<false, W1>(v[0][0], v[0][1], rs, 64, lane8, hi8, true, true);
+    __builtin_amdgcn_sched_barrier(0);
+    tri2_load_blk<false, 16>(v[1][0], v[1][1], rs, 48, lane8, hi8, true, false);
+    __builtin_amdgcn_sched_barrier(0);
+    dpp_diag<false, W1, 0x1, 0>(r[1], v[0][1]);
+    asm volatile("s_nop 1");
+    x64[lane] = r[1];
+    wave_sync();
+    {
+        const double x = x64[xl];
+        dpp_off<false, W1, 0xF, 0>(r[0], x, v[0][0]);
+    }
+    wave_sync();
+    auto bwd_blk = [&](auto B_, auto BUF_) {
+        constexpr int B = decltype(B_)::value, BUF = decltype(BUF_)::value;
+        double (&f0)[16] = v[BUF][0];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (B > 0) tri2_load_blk<false, 16>(v[BUF ^ 1][0], v[BUF ^ 1][1], rs, 16 * (B - 1), lane8, hi8, true, false);
+        __builtin_amdgcn_sched_barrier(0);
+        dpp_diag<false, 16, 1 << B, 0>(r[0], f0);
+        if constexpr (B > 0) {
+            asm volatile("s_nop 1");
+            x64[lane] = r[0];
+            wave_sync();
+            const double x = x64[16 * B + xl];
+            dpp_off<false, 16, (1 << B) - 1, 0>(r[0], x, f0);
+            wave_sync();
+        }
+    };
+    bwd_blk(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{});
+    bwd_blk(std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{});
+    bwd_blk(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+    bwd_blk(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    asm volatile("s_nop 1");
+}
+
 template <int NMAX>
 __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* scr, int n, int lane,
                                           const int (&perm)[2], double (&b)[2]) {
@@ -1661,6 +1759,21 @@ __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* s
     wave_sync();
     double r[2] = {dsc[perm[0]], dsc[perm[1]]};   // P b
     wave_sync();
+#if BR_TRI_DPP
+    if constexpr (NMAX > 64 && NMAX <= 72) {
+        // (all solve loads are buffer loads: drain first so the waitcnt pass can count them in order)
+        __builtin_amdgcn_s_waitcnt(0x70);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * JW * 8, 0x00020000);
+        const double dv[2] = {
+            __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * JW * 8, 0)),
+            __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8 + 512, NMAX * JW * 8, 0))};
+        tri_sweeps2_dpp<NMAX>(rs, lane, r, dv, scr);
+        b[0] = (lane < n) ? r[0] : 0.0;
+        b[1] = (lane + 64 < n) ? r[1] : 0.0;
+        return;
+    }
+#endif
 #if BR_TRI_DIAG
     tri_sweep2_diag<true, NMAX>(wsg, lane, n, r);
 #else
