@@ -125,7 +125,8 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
 // ------------------------------------------------------------------------------------
 // sub-phase shader clocks (diagnostic build, BR_PHASE_CLOCKS): BR_SUB_T(t) starts a timer,
 // BR_SUB_ADD(slot, t) adds its cycles to g_sub[slot] (one atomic from lane 0); read and reset
-// from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather.
+// from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather,
+// 3..6 gas-only Jacobian: column-pass setup, entry loop, column writes, multipliers.
 // ------------------------------------------------------------------------------------
 #if BR_PHASE_CLOCKS
 __device__ unsigned long long g_sub[8];
@@ -576,6 +577,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
     }
     const double Ctot = wave_sum(cg);
     wave_sync();
+    BR_SUB_T(jt0);
     if (MF(nset)) {
         third_body_sets<CPL>(M, tb, R.sp, Ctot, lane);
         wave_sync();
@@ -624,12 +626,16 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
         // in col_rx), so 18 passes with 3 wave barriers each instead of 53 for GRI
         double* mcb = R.sp + L::MC;
         const int n = MF(n);
+        BR_SUB_ADD(6, jt0);
 #pragma unroll 1
         for (int j0 = 0; j0 < n; j0 += 3) {
+            BR_SUB_T(jt1);
             if (lane < n) { accw[lane] = 0.0; accs[lane] = 0.0; mcb[lane] = 0.0; }
             wave_sync();
             const int* cp = MF(col_ptr);
             const int cb = cp[j0], c1 = cp[min(j0 + 1, n)], c2 = cp[min(j0 + 2, n)], ce = cp[min(j0 + 3, n)];
+            BR_SUB_ADD(3, jt1);
+            BR_SUB_T(jt2);
 #pragma unroll 1
             for (int i = cb + lane; i < ce; i += WAVE) {
                 const int r = MF(col_rx)[i];
@@ -658,6 +664,8 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                 scatter(acc, rec[4], rec[5], rec[6], d);
             }
             wave_sync();
+            BR_SUB_ADD(4, jt2);
+            BR_SUB_T(jt3);
             const double Mk = tb.molwt[lane];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -669,6 +677,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                 }
             }
             wave_sync();
+            BR_SUB_ADD(5, jt3);
         }
         return;
     }
