@@ -459,6 +459,7 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL> V, int lane, int 
 template <int CPL>
 __device__ __forceinline__ void begin_step(LCtl* C, VA<CPL> V, int lane, const CtlArgs& a) {
     constexpr int VW = 64 * CPL;
+    BR_SUB_T(bt0);
 #pragma unroll
     FOR_S {
         const double z0 = V[CS];
@@ -475,6 +476,7 @@ __device__ __forceinline__ void begin_step(LCtl* C, VA<CPL> V, int lane, const C
         cv_rescale<CPL>(C, V, lane);
     }
     begin_attempt<CPL>(C, V, lane, FIRST_CALL);
+    BR_SUB_ADD(7, bt0);
 }
 
 // Controller, part 1: after the RHS value f = F(y) of this lane is known.
@@ -1933,11 +1935,13 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
 // diagnostic build only (not declared in brhip.h): read and reset the sub-phase clock sums
 // (BR_SUB_ADD slots of brhip_device.hpp)
 extern "C" int br_diag_sub(double* out8) {
-    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(brhip::g_sub), sizeof(v)) != hipSuccess) return -1;
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(brhip::g_sub), z, sizeof(z)) != hipSuccess) return -1;
-    for (int i = 0; i < 8; ++i) out8[i] = (double)v[i];
+    std::vector<unsigned long long> v((size_t)brhip::SUB_MAXW * 8, 0ull);
+    if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(brhip::g_sub), v.size() * 8) != hipSuccess) return -1;
+    for (int i = 0; i < 8; ++i) out8[i] = 0.0;
+    for (size_t w = 0; w < (size_t)brhip::SUB_MAXW; ++w)
+        for (int i = 0; i < 8; ++i) out8[i] += (double)v[w * 8 + i];
+    std::fill(v.begin(), v.end(), 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(brhip::g_sub), v.data(), v.size() * 8) != hipSuccess) return -1;
     return 0;
 }
 #endif

@@ -126,12 +126,20 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
 // sub-phase shader clocks (diagnostic build, BR_PHASE_CLOCKS): BR_SUB_T(t) starts a timer,
 // BR_SUB_ADD(slot, t) adds its cycles to g_sub[slot] (one atomic from lane 0); read and reset
 // from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather,
-// 3..6 gas-only Jacobian: column-pass setup, entry loop, column writes, multipliers.
+// 3..6 gas-only Jacobian: column-pass setup, entry loop, column writes, multipliers; 7 begin_step.
 // ------------------------------------------------------------------------------------
 #if BR_PHASE_CLOCKS
-__device__ unsigned long long g_sub[8];
+// one row of 8 sums per resident wave (plain adds by the wave's lane 0: one device-wide atomic
+// counter hit by every wave at every step saturated the memory-side atomic unit and slowed the
+// whole kernel 2x)
+constexpr int SUB_MAXW = 16384;
+__device__ unsigned long long g_sub[SUB_MAXW][8];
+__device__ __forceinline__ void sub_add(int slot, unsigned long long dt) {
+    const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < SUB_MAXW) g_sub[w][slot] += dt;
+}
 #define BR_SUB_T(t) const unsigned long long t = clock64()
-#define BR_SUB_ADD(slot, t) do { if ((threadIdx.x & 63) == 0) atomicAdd(&::brhip::g_sub[slot], clock64() - (t)); } while (0)
+#define BR_SUB_ADD(slot, t) ::brhip::sub_add(slot, clock64() - (t))
 #else
 #define BR_SUB_T(t)
 #define BR_SUB_ADD(slot, t)
