@@ -1398,6 +1398,50 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         for (int c = 0; c < 3; ++c) spar[4 * (size_t)r + c] = d->s_arr[r * 3 + c];
         spar[4 * (size_t)r + 3] = g >= 0 ? d->molwt[g] : 1.0;
     }
+    // ---- scatter-slot order: the production sums are accumulated with one LDS atomic instruction per
+    //      list slot e over the 64 reactions of a pass (lanes), so a species that sits in the same
+    //      slot of many of those reactions serialises that instruction (LDS address conflicts; GRI's
+    //      H, O, OH, H2O ...). Per group of 64 reactions, each reaction's list is permuted so that its
+    //      species land in the slots where they are least used so far (greedy, exhaustive over the
+    //      <= 720 orders of one list). Only the order of the per-species sums changes.
+    auto spread_slots = [](std::vector<uint32_t>& recs, int words, int off, int nrec) {
+        for (int g0 = 0; g0 < nrec; g0 += WAVE) {
+            static thread_local int cnt[6][256];
+            memset(cnt, 0, sizeof(cnt));
+            for (int i = g0; i < std::min(nrec, g0 + WAVE); ++i) {
+                uint32_t* w = &recs[(size_t)words * i + off];
+                const int m = (w[1] >> 16) & 255;
+                int sp[6], nu[6], ord[6], best[6];
+                for (int e = 0; e < m; ++e) {
+                    sp[e] = e < 4 ? (w[0] >> (8 * e)) & 255 : (w[1] >> (8 * (e - 4))) & 255;
+                    nu[e] = ((int)(w[2] << (28 - 4 * e))) >> 28;
+                    ord[e] = e;
+                }
+                long bc = -1;
+                do {   // ord[slot] = entry placed in that slot
+                    long c = 0;
+                    for (int t = 0; t < m; ++t) { const long v = cnt[t][sp[ord[t]]] + 1; c += v * v; }
+                    if (bc < 0 || c < bc) { bc = c; std::copy(ord, ord + m, best); }
+                } while (std::next_permutation(ord, ord + m));
+                uint32_t w0 = 0, w1 = w[1] & ~0xFFFFu, w2 = w[2] & 0xFF000000u;
+                for (int t = 0; t < m; ++t) {
+                    const int e = best[t];
+                    if (t < 4) w0 |= (uint32_t)sp[e] << (8 * t);
+                    else w1 |= (uint32_t)sp[e] << (8 * (t - 4));
+                    w2 |= (uint32_t)(nu[e] & 15) << (4 * t);
+                    cnt[t][sp[e]]++;
+                }
+                w[0] = w0; w[1] = w1; w[2] = w2;
+            }
+        }
+    };
+    {
+        const char* ss = getenv("BRHIP_SPREAD");   // "0": lists in first-appearance order (A/B)
+        if (!(ss && atoi(ss) == 0)) {
+            spread_slots(rx, RX_WORDS, 4, nrg);
+            spread_slots(sx, SX_WORDS, 6, nrs);
+        }
+    }
     // ---- Jacobian column lists: reactions whose rate depends on component j
     std::vector<int> colptr(1, 0), colrx;
     for (int j = 0; j < n; ++j) {
@@ -1435,7 +1479,15 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         for (int k = 0; k < SPW; ++k) { mw[k] = 1.0; mw[SPW + k] = 1.0; }
         for (int k = 0; k < ng; ++k) mw[k] = d->molwt[k];
         for (int i = 0; i < ns; ++i) mw[SPW + ng + i] = d->sigma ? d->sigma[i] : 1.0;
-        if (nrg) memcpy(img.data() + IMG_RX_OFF, rx.data(), rx.size() * 4);
+        if (nrg) {
+#if BR_RX_SPLIT
+            uint32_t* ra = reinterpret_cast<uint32_t*>(img.data() + IMG_RX_OFF);
+            for (int i = 0; i < nrg; ++i)
+                for (int w = 0; w < RX_WORDS; ++w) ra[(w < 4 ? 4 * i : 4 * nrg + 4 * i) + (w & 3)] = rx[(size_t)RX_WORDS * i + w];
+#else
+            memcpy(img.data() + IMG_RX_OFF, rx.data(), rx.size() * 4);
+#endif
+        }
         if (nrs) memcpy(img.data() + M.sx_off, sx.data(), sx.size() * 4);
         if (nrs) memcpy(img.data() + M.sxe_off, sxe.data(), sxe.size() * 8);
         if (!tbs.empty()) memcpy(img.data() + M.tbs_off, tbs.data(), tbs.size() * 4);

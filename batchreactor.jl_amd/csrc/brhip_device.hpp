@@ -65,6 +65,25 @@ __device__ __forceinline__ T karg_field(size_t off) {
     return *(cT*)(p + off);
 }
 #define MF(f) (::brhip::karg_field<decltype(::brhip::DevMech::f)>(offsetof(::brhip::DevMech, f)))
+// RX records in the image: split (BR_RX_SPLIT = 1) into words 0..3 of every reaction, then words
+// 4..7 (two arrays with a 16-byte stride: the b128 record reads of 64 consecutive reactions hit
+// every LDS bank once; with the 32-byte stride of whole records two lanes share each bank)
+#ifndef BR_RX_SPLIT
+#define BR_RX_SPLIT 1
+#endif
+template <class P>
+struct RxRec {
+    P a, b;
+    __device__ __forceinline__ uint32_t operator[](int w) const { return w < 4 ? a[w] : b[w - 4]; }
+};
+template <class P>
+__device__ __forceinline__ RxRec<P> rx_rec(P rx, int r) {
+#if BR_RX_SPLIT
+    return {rx + 4 * r, rx + 4 * MF(nrg) + 4 * r};
+#else
+    return {rx + 8 * r, rx + 8 * r + 4};
+#endif
+}
 
 // RX record: w0 reactant species (4 x 8 bit; pad = SP_ONE, a slot holding 1.0, so the
 // concentration products need no branches), w1 product species, w2 info (third-body
@@ -304,7 +323,7 @@ __device__ __forceinline__ void init_tconst(const DevMech& M, const Tab& tb, con
     const double RT = R_GAS * T;
 #pragma unroll 1
     for (int r = lane; r < MF(nrg); r += WAVE) {
-        const uint32_t* rec = tb.rx + RX_WORDS * r;
+        const auto rec = rx_rec(tb.rx, r);
         const uint32_t info = rec[2];
         const double* gp = MF(g_par) + 4 * r;
         const double kf = gp[0] * exp(gp[1] * lT - gp[2] / T);
@@ -472,10 +491,11 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
         const double2 k0 = kn0, k1 = has1 ? kn1 : kn0;
         if (r + 2 * WAVE < nrg) kn0 = kpair(R.rxd, r + 2 * WAVE);
         if (r + 3 * WAVE < nrg) kn1 = kpair(R.rxd, r + 3 * WAVE);
-        const uint4 ra0 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r);
-        const uint4 rb0 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * r + 4);
-        const uint4 ra1 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * q1);
-        const uint4 rb1 = *reinterpret_cast<const uint4*>(tb.rx + RX_WORDS * q1 + 4);
+        const auto rr0 = rx_rec(tb.rx, r), rr1 = rx_rec(tb.rx, q1);
+        const uint4 ra0 = *reinterpret_cast<const uint4*>(rr0.a);
+        const uint4 rb0 = *reinterpret_cast<const uint4*>(rr0.b);
+        const uint4 ra1 = *reinterpret_cast<const uint4*>(rr1.a);
+        const uint4 rb1 = *reinterpret_cast<const uint4*>(rr1.b);
         const double D0 = rate(r, ra0, k0);
         const double D1 = rate(q1, ra1, k1);
         scatter(accw, rb0.x, rb0.y, rb0.z, D0);
@@ -592,7 +612,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
     }
 #pragma unroll 1
     for (int r = lane; r < MF(nrg); r += WAVE) {                   // per-reaction multipliers
-        const uint32_t* rec = tb.rx + RX_WORDS * r;
+        const auto rec = rx_rec(tb.rx, r);
         const uint32_t info = rec[2];
         const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
         const double kf = R.rxd[2 * r], kr = R.rxd[2 * r + 1];
@@ -649,7 +669,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                 const int r = MF(col_rx)[i];
                 const int j = j0 + (i >= c1) + (i >= c2);
                 double* acc = (i >= c2) ? mcb : (i >= c1) ? accs : accw;
-                const uint32_t* rec = tb.rx + RX_WORDS * r;
+                const auto rec = rx_rec(tb.rx, r);
                 const uint32_t info = rec[2];
                 const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
                 const double pre = ld_l2(jscr + 2 * r);
@@ -703,7 +723,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
             const int rr = MF(col_rx)[i];
             if (rr < MF(nrg)) {
                 const int r = rr;
-                const uint32_t* rec = tb.rx + RX_WORDS * r;
+                const auto rec = rx_rec(tb.rx, r);
                 const uint32_t info = rec[2];
                 const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
                 const double pre = ld_l2(jscr + 2 * r);

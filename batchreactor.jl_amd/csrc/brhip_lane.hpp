@@ -859,7 +859,8 @@ __device__ __forceinline__ void lane_tconst(const LaneLay& LL, double* Lp, const
     const double RT = R_GAS * T;
     const CU32* rx = (const CU32*)((const char*)MF(img) + Lay<1>::IMG_RX);
     for (int r = 0; r < nrg; ++r) {
-        const uint32_t w0 = rx[RX_WORDS * r], w1 = rx[RX_WORDS * r + 1], info = rx[RX_WORDS * r + 2];
+        const auto rq = rx_rec(rx, r);
+        const uint32_t w0 = rq[0], w1 = rq[1], info = rq[2];
         const CF64* gp = (const CF64*)MF(g_par) + 4 * r;
         const double kf = gp[0] * exp(gp[1] * lT - gp[2] / T);
         double kr = 0.0;
@@ -936,7 +937,7 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
         kq[d][1] = G.ld(LL.g_rxd + 2 * rr + 1);
     }
     for (int r = 0; r < nrg; ++r) {
-        const CU32* rec = rx + RX_WORDS * r;
+        const auto rec = rx_rec(rx, r);
         const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], s0 = rec[4], s1 = rec[5], s2 = rec[6];
         const double kf = kq[0][0], kr = kq[0][1];
 #pragma unroll
@@ -1003,7 +1004,7 @@ __device__ __forceinline__ void lane_jac(const LaneLay& LL, const double* Lp, co
 #pragma unroll
         for (int i = 0; i < NM; ++i) G.st(j * NM + i, 0.0);
     for (int r = 0; r < nrg; ++r) {
-        const CU32* rec = rx + RX_WORDS * r;
+        const auto rec = rx_rec(rx, r);
         const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], s0 = rec[4], s1 = rec[5], s2 = rec[6];
         const double kf = G.ld(LL.g_rxd + 2 * r), kr = G.ld(LL.g_rxd + 2 * r + 1);
         double cf[4], cb[4];
