@@ -1461,7 +1461,26 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         }
         colptr.push_back((int)colrx.size());
     }
-    // ---- LDS table image: molwt[SPW] | sigma[SPW] | RX | SX | SXE | TBE
+    // ---- gas-only fast Jacobian (jacobian_fast): reactant / product column lists (no third-body
+    //      entries: that dependence goes through the efficiency sets), staged in the LDS image
+    std::vector<int> cmp(1, 0);
+    std::vector<uint16_t> cmr;
+    const char* jf_env = getenv("BRHIP_JFAST");   // "0": the general column-list Jacobian (A/B)
+    const bool jfast = (ns == 0) && (M.cpl == 1) && (M.nset <= JF_MAXSET) && (ntb <= WAVE) && (nrg < 65536) &&
+                       !(jf_env && atoi(jf_env) == 0);
+    if (jfast) {
+        for (int j = 0; j < n; ++j) {
+            for (int i = 0; i < nrg; ++i) {
+                const int r = perm[i];
+                bool dep = false;
+                for (int e = 0; e < d->g_nf[r]; ++e) dep |= d->g_f[r * 4 + e] == j;
+                for (int e = 0; e < d->g_nr[r]; ++e) dep |= d->g_r[r * 4 + e] == j;
+                if (dep) cmr.push_back((uint16_t)i);
+            }
+            cmp.push_back((int)cmr.size());
+        }
+    }
+    // ---- LDS table image: molwt[SPW] | sigma[SPW] | RX | SX | SXE | TBE | TBS | CMP | CMR
     auto al16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     size_t off = IMG_RX_OFF + al16(RX_WORDS * 4 * (size_t)nrg);
     M.sx_off = (int)off;
@@ -1472,6 +1491,26 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     off += al16(16 * tbe.size());
     M.tbs_off = (int)off;
     off += al16(4 * tbs.size());
+    M.jfast = jfast ? 1 : 0;
+    M.ntbr = ntb;
+    M.cmp_off = (int)off;
+    off += jfast ? al16(4 * cmp.size()) : 0;
+    M.cmr_off = (int)off;
+    off += jfast ? al16(2 * cmr.size()) : 0;
+    // per gas species, the efficiency sets with eff != 1 (jacobian_fast's third-body columns)
+    std::vector<int> tjp(1, 0);
+    std::vector<std::pair<int, double>> tje;
+    if (jfast) {
+        for (int j = 0; j < n; ++j) {
+            for (size_t q = 0; q < sets.size(); ++q)
+                if (j < ng && sets[q][j] != 1.0) tje.push_back({(int)q, sets[q][j] - 1.0});
+            tjp.push_back((int)tje.size());
+        }
+    }
+    M.tjp_off = (int)off;
+    off += jfast ? al16(4 * tjp.size()) : 0;
+    M.tje_off = (int)off;
+    off += jfast ? al16(16 * tje.size()) : 0;
     M.img_bytes = (int)al16(off);
     std::vector<unsigned char> img(M.img_bytes, 0);
     {
@@ -1491,6 +1530,15 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         if (nrs) memcpy(img.data() + M.sx_off, sx.data(), sx.size() * 4);
         if (nrs) memcpy(img.data() + M.sxe_off, sxe.data(), sxe.size() * 8);
         if (!tbs.empty()) memcpy(img.data() + M.tbs_off, tbs.data(), tbs.size() * 4);
+        if (jfast) {
+            memcpy(img.data() + M.cmp_off, cmp.data(), cmp.size() * 4);
+            if (!cmr.empty()) memcpy(img.data() + M.cmr_off, cmr.data(), cmr.size() * 2);
+            memcpy(img.data() + M.tjp_off, tjp.data(), tjp.size() * 4);
+            for (size_t q = 0; q < tje.size(); ++q) {
+                memcpy(img.data() + M.tje_off + 16 * q, &tje[q].first, 4);
+                memcpy(img.data() + M.tje_off + 16 * q + 8, &tje[q].second, 8);
+            }
+        }
         for (size_t i = 0; i < tbe.size(); ++i) {
             unsigned char* e = img.data() + M.tbe_off + 16 * i;
             const int sp = tbe[i].first;

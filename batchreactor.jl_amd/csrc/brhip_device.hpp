@@ -50,6 +50,13 @@ struct DevMech {
     const double* tb_eff;         // [nset][n] dense efficiencies
     const int* col_ptr;           // [n+1] Jacobian column lists
     const int* col_rx;            // combined reaction index (gas r, surface nrg+r)
+    // gas-only fast Jacobian (jfast): mass-action column lists in the LDS image (cmp_off: int
+    // [n+1] column starts, cmr_off: uint16 reaction per entry; reactant / product dependence
+    // only), third-body dependence through the efficiency sets (ntb third-body reactions first)
+    int jfast, ntbr, cmp_off, cmr_off;
+    // per gas species j, the efficiency sets with eff_j != 1: tjp_off int [n+1] starts, tje_off
+    // 16-byte entries {int set, pad, double eff - 1}
+    int tjp_off, tje_off;
 };
 
 // The kernels' first argument is the DevMech (kernarg offset 0). The hot-path functions re-read
@@ -295,6 +302,25 @@ __device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, u
             lds_add(&acc[k], (double)nu * v);                    // exact for small integer nu
         }
     }
+}
+
+// scatter() except for species `self`: its nu * v is returned instead of added (the caller sums
+// it in a register and reduces over the wave: in a Jacobian column pass nearly every entry of
+// column j touches species j, which made acc[j] the hot address of every atomic slot)
+__device__ __forceinline__ double scatter_noself(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, double v, int self) {
+    const int cnt = (w1 >> 16) & 255;
+    double sv = 0.0;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        if (e < cnt) {
+            const int k = e < 4 ? sp8(w0, e) : sp8(w1, e - 4);
+            const int nu = ((int)(w2 << (28 - 4 * e))) >> 28;
+            const double t = (double)nu * v;
+            if (k == self) sv += t;
+            else lds_add(&acc[k], t);
+        }
+    }
+    return sv;
 }
 
 // stage the table image (all threads of the workgroup), then barrier
@@ -579,6 +605,153 @@ __device__ __forceinline__ void rhs(const DevMech& M, const Tab& tb_, const RVie
 __device__ __forceinline__ double ld_l2(const BR_GLOBAL double* p) {
     return __hip_atomic_load((const double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Gas-only analytic Jacobian (DevMech::jfast), after the multiplier loop of jacobian() left
+// jscr[2r] = pre_r and jscr[2r+1] = D_r d(pre_r)/d[M] (pre = [M] or the falloff factor):
+//   dq_r/dc_j = pre_r (kf_r d(prod_f)/dc_j - kr_r d(prod_b)/dc_j) + D_r dpre_r/d[M] eff_{s(r),j}.
+// The third-body term is a product over the efficiency sets s: with w_s[k] = sum over the
+// third-body reactions r of set s of nu_kr D_r dpre_r/d[M], its contribution to J[k][j] is
+// sum_s w_s[k] eff_{s,j}: nset scatter passes and nset FMAs per entry (efficiencies by scalar
+// loads) instead of a column-list entry for every (third-body reaction, species) pair. The
+// mass-action part runs over reactant / product column lists staged in the LDS image, with
+// (pre kf, pre kr) as one 16-byte load per entry, issued an iteration ahead.
+constexpr int JF_MAXSET = 16;
+__device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int lane, bool xm, BR_GLOBAL double* Jsave,
+                                              BR_GLOBAL double* jscr) {
+    BR_SUB_T(jc0);
+    typedef Lay<1> L;
+    const double* conc = R.sp + L::CONC;
+    double* accw = R.sp + L::ACCW;
+    double* accs = R.sp + L::ACCS;
+    double* mcb = R.sp + L::MC;
+    const int n = MF(n), nset = MF(nset), ntb = MF(ntbr);
+    // per-reaction multipliers: jscr[2r] = pre kf, jscr[2r+1] = pre kr; D dpre/d[M] of the
+    // third-body reaction on this lane (r = lane < ntb <= 64: third-body reactions come first)
+    double dcm = 0.0;
+#pragma unroll 1
+    for (int r = lane; r < MF(nrg); r += WAVE) {
+        const auto rec = rx_rec(tb.rx, r);
+        const uint32_t info = rec[2];
+        const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
+        const double kf = R.rxd[2 * r], kr = R.rxd[2 * r + 1];
+        double pre = 1.0;
+        if (tbk) {
+            double Pf = 1.0, Pb = 1.0;
+            for (int e = 0; e < 4; ++e) if (e < nf) Pf *= conc[sp8(rec[0], e)];
+            for (int e = 0; e < 4; ++e) if (e < nr) Pb *= conc[sp8(rec[1], e)];
+            const double D = kf * Pf - kr * Pb;
+            const double Mc = R.sp[L::MC + gi_tbidx(info)];
+            double coefM;
+            if (tbk == 1) { pre = Mc; coefM = 1.0; }
+            else {
+                double fac, dfac;
+                falloff<true>(R.fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
+                pre = fac * (xm ? Mc * 1e-6 : 1.0);
+                coefM = dfac * (xm ? Mc * 1e-6 : 1.0) + (xm ? fac * 1e-6 : 0.0);
+            }
+            dcm = D * coefM;
+        }
+        jscr[2 * r] = pre * kf;
+        jscr[2 * r + 1] = pre * kr;
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // scratch stores complete before other lanes read them
+    wave_sync();
+    // w_s[lane] for every efficiency set
+    double w[JF_MAXSET];
+    const auto recl = rx_rec(tb.rx, lane < ntb ? lane : 0);
+    const uint32_t tbset = gi_tbidx(recl[2]);
+#pragma unroll
+    for (int st = 0; st < JF_MAXSET; ++st) {
+        w[st] = 0.0;
+        if (st < nset) {
+            if (lane < n) accw[lane] = 0.0;
+            wave_sync();
+            if (lane < ntb && (int)tbset == st) scatter(accw, recl[4], recl[5], recl[6], dcm);
+            wave_sync();
+            w[st] = (lane < n) ? accw[lane] : 0.0;
+            wave_sync();
+        }
+    }
+    BR_SUB_ADD(6, jc0);
+    const int* cp = reinterpret_cast<const int*>(reinterpret_cast<const char*>(br_lds) + MF(cmp_off));
+    const uint16_t* cr = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(br_lds) + MF(cmr_off));
+    const int* tjp = reinterpret_cast<const int*>(reinterpret_cast<const char*>(br_lds) + MF(tjp_off));
+    const char* tje = reinterpret_cast<const char*>(br_lds) + MF(tje_off);
+    // third-body part of J[k][j] = sum_s w_s[k] eff_{s,j} = wsum[k] + sum over the sets with
+    // eff_{s,j} != 1 of w_s[k] (eff_{s,j} - 1): no efficiency loads for the other columns
+    double wsum = 0.0;
+#pragma unroll
+    for (int st = 0; st < JF_MAXSET; ++st) if (st < nset) wsum += w[st];
+    const double Mk = tb.molwt[lane];
+#pragma unroll 1
+    for (int j0 = 0; j0 < n; j0 += 3) {
+        if (lane < n) { accw[lane] = 0.0; accs[lane] = 0.0; mcb[lane] = 0.0; }
+        const int cb = uni(cp[j0]), c1 = uni(cp[min(j0 + 1, n)]), c2 = uni(cp[min(j0 + 2, n)]), ce = uni(cp[min(j0 + 3, n)]);
+        wave_sync();
+        BR_SUB_T(je0);
+        double sf0 = 0.0, sf1 = 0.0, sf2 = 0.0;   // d(nu_j q)/dc_j of the entries of columns j0 .. j0+2
+        int i = cb + lane;
+        int r = (i < ce) ? (int)cr[i] : 0;
+        // (L1-bypassing loads: other lanes wrote these in this call; the slot's L1 lines may be stale)
+        double2 pk = (i < ce) ? make_double2(ld_l2(jscr + 2 * r), ld_l2(jscr + 2 * r + 1)) : make_double2(0.0, 0.0);
+#pragma unroll 1
+        for (; i < ce; i += WAVE) {
+            const int in = i + WAVE;
+            const int rn = (in < ce) ? (int)cr[in] : 0;
+            const double2 pkn = (in < ce) ? make_double2(ld_l2(jscr + 2 * rn), ld_l2(jscr + 2 * rn + 1)) : make_double2(0.0, 0.0);
+            const int j = j0 + (i >= c1) + (i >= c2);
+            double* acc = (i >= c2) ? mcb : (i >= c1) ? accs : accw;
+            const auto rec = rx_rec(tb.rx, r);
+            const uint32_t info = rec[2];
+            const int nf = gi_nf(info), nr = gi_nr(info);
+            double d = 0.0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (e < nf && sp8(rec[0], e) == j) {
+                double pr = pk.x;
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nf) pr *= conc[sp8(rec[0], e2)];
+                d += pr;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (e < nr && sp8(rec[1], e) == j) {
+                double pr = pk.y;
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= conc[sp8(rec[1], e2)];
+                d -= pr;
+            }
+            const double sv = scatter_noself(acc, rec[4], rec[5], rec[6], d, j);
+            if (i >= c2) sf2 += sv;
+            else if (i >= c1) sf1 += sv;
+            else sf0 += sv;
+            r = rn;
+            pk = pkn;
+        }
+        wave_sync();
+        BR_SUB_ADD(4, je0);
+        BR_SUB_T(je1);
+        const double st0 = wave_sum(sf0), st1 = wave_sum(sf1), st2 = wave_sum(sf2);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int j = j0 + c;
+            if (j < n) {
+                const double* acc = c == 0 ? accw : c == 1 ? accs : mcb;
+                double v = (lane < n ? acc[lane] : 0.0) + wsum;
+                if (lane == j) v += (c == 0 ? st0 : c == 1 ? st1 : st2);
+                const int t0 = uni(tjp[j]), t1 = uni(tjp[j + 1]);
+                for (int e = t0; e < t1; ++e) {
+                    const int se = uni(*reinterpret_cast<const int*>(tje + 16 * e));
+                    double ws = 0.0;
+#pragma unroll
+                    for (int st = 0; st < JF_MAXSET; ++st) ws = (st == se) ? w[st] : ws;
+                    v = fma(ws, *reinterpret_cast<const double*>(tje + 16 * e + 8), v);
+                }
+                Jsave[j * WAVE + lane] = (lane < n) ? Mk * v / tb.molwt[j] : 0.0;
+            }
+        }
+        wave_sync();
+        BR_SUB_ADD(5, je1);
+    }
+}
+
 template <int CPL>
 __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const RView& R_, double T, double Asv,
                                          double Asv_th, const double (&u)[CPL], int lane, double* Jsave_,
@@ -609,6 +782,12 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
     if (MF(nset)) {
         third_body_sets<CPL>(M, tb, R.sp, Ctot, lane);
         wave_sync();
+    }
+    if constexpr (CPL == 1) {
+        if (MF(jfast)) {
+            jacobian_fast(tb, R, lane, xm, Jsave, jscr);
+            return;
+        }
     }
 #pragma unroll 1
     for (int r = lane; r < MF(nrg); r += WAVE) {                   // per-reaction multipliers
