@@ -682,6 +682,17 @@ __device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int
 #pragma unroll
     for (int st = 0; st < JF_MAXSET; ++st) if (st < nset) wsum += w[st];
     const double Mk = tb.molwt[lane];
+    const double rMl = 1.0 / tb.molwt[lane];   // 1/M_j, broadcast from lane j for column j
+    // (L1-bypassing loads: other lanes wrote the multipliers in this call; the slot's L1 lines may
+    // be stale.) The first entry of every pass is fetched while the previous pass writes its
+    // columns, so no pass starts on a full L2 round trip.
+    auto fetch = [&](int i, int ce, int& r, double2& pk) {
+        r = (i < ce) ? (int)cr[i] : 0;
+        pk = (i < ce) ? make_double2(ld_l2(jscr + 2 * r), ld_l2(jscr + 2 * r + 1)) : make_double2(0.0, 0.0);
+    };
+    int rq;
+    double2 pq;
+    fetch(uni(cp[0]) + lane, uni(cp[min(3, n)]), rq, pq);
 #pragma unroll 1
     for (int j0 = 0; j0 < n; j0 += 3) {
         if (lane < n) { accw[lane] = 0.0; accs[lane] = 0.0; mcb[lane] = 0.0; }
@@ -690,9 +701,8 @@ __device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int
         BR_SUB_T(je0);
         double sf0 = 0.0, sf1 = 0.0, sf2 = 0.0;   // d(nu_j q)/dc_j of the entries of columns j0 .. j0+2
         int i = cb + lane;
-        int r = (i < ce) ? (int)cr[i] : 0;
-        // (L1-bypassing loads: other lanes wrote these in this call; the slot's L1 lines may be stale)
-        double2 pk = (i < ce) ? make_double2(ld_l2(jscr + 2 * r), ld_l2(jscr + 2 * r + 1)) : make_double2(0.0, 0.0);
+        int r = rq;
+        double2 pk = pq;
 #pragma unroll 1
         for (; i < ce; i += WAVE) {
             const int in = i + WAVE;
@@ -728,6 +738,7 @@ __device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int
         wave_sync();
         BR_SUB_ADD(4, je0);
         BR_SUB_T(je1);
+        if (j0 + 3 < n) fetch(uni(cp[j0 + 3]) + lane, uni(cp[min(j0 + 6, n)]), rq, pq);
         const double st0 = wave_sum(sf0), st1 = wave_sum(sf1), st2 = wave_sum(sf2);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -744,7 +755,7 @@ __device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int
                     for (int st = 0; st < JF_MAXSET; ++st) ws = (st == se) ? w[st] : ws;
                     v = fma(ws, *reinterpret_cast<const double*>(tje + 16 * e + 8), v);
                 }
-                Jsave[j * WAVE + lane] = (lane < n) ? Mk * v / tb.molwt[j] : 0.0;
+                Jsave[j * WAVE + lane] = (lane < n) ? Mk * v * bcast(rMl, j) : 0.0;
             }
         }
         wave_sync();
