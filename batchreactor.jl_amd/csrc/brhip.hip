@@ -1018,7 +1018,9 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         }
         double b[CPL];
         BR_CLK(c2);
+        BR_SUB_T(pr0);
         int act_code = ctl_post_rhs<CPL>(C, V, lane, f, b);
+        BR_SUB_ADD(3, pr0);
         BR_ACC(cyc_ctl, c2);
         if (act_code == A_RHS) continue;
         if (act_code == A_DONE) break;

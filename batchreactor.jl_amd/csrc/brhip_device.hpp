@@ -152,7 +152,8 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
 // sub-phase shader clocks (diagnostic build, BR_PHASE_CLOCKS): BR_SUB_T(t) starts a timer,
 // BR_SUB_ADD(slot, t) adds its cycles to g_sub[slot] (one atomic from lane 0); read and reset
 // from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather,
-// 3..6 gas-only Jacobian: column-pass setup, entry loop, column writes, multipliers; 7 begin_step.
+// 3 ctl_post_rhs, 4..6 gas-only Jacobian: entry loop, column writes, multipliers (+ set passes);
+// 7 begin_step.
 // ------------------------------------------------------------------------------------
 #if BR_PHASE_CLOCKS
 // one row of 8 sums per resident wave (plain adds by the wave's lane 0: one device-wide atomic
@@ -847,12 +848,10 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
         BR_SUB_ADD(6, jt0);
 #pragma unroll 1
         for (int j0 = 0; j0 < n; j0 += 3) {
-            BR_SUB_T(jt1);
             if (lane < n) { accw[lane] = 0.0; accs[lane] = 0.0; mcb[lane] = 0.0; }
             wave_sync();
             const int* cp = MF(col_ptr);
             const int cb = cp[j0], c1 = cp[min(j0 + 1, n)], c2 = cp[min(j0 + 2, n)], ce = cp[min(j0 + 3, n)];
-            BR_SUB_ADD(3, jt1);
             BR_SUB_T(jt2);
 #pragma unroll 1
             for (int i = cb + lane; i < ce; i += WAVE) {

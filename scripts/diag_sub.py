@@ -19,7 +19,7 @@ from bench import CONFIGS, make_mech  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "gri"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
 SLOTS = {0: ("LU panel 1", "nsetups"), 1: ("LU panel 2", "nsetups"), 2: ("LU gather", "nsetups"),
-         6: ("J multipliers", "nje"), 3: ("J pass setup", "nje"), 4: ("J entries", "nje"), 5: ("J col write", "nje"),
+         6: ("J multipliers", "nje"), 3: ("ctl post_rhs", "nfe"), 4: ("J entries", "nje"), 5: ("J col write", "nje"),
          7: ("ctl begin_step", "nsteps")}
 mech = make_mech(pkg, cfg)
 eng = pkg.Engine(mech)
