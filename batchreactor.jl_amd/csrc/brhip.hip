@@ -209,18 +209,22 @@ template <int CPL>
 __device__ __forceinline__ double mole_frac_of(const double (&v)[CPL], int lane, int k) {
     const double* mw = reinterpret_cast<const double*>(br_lds);   // staged molwt[] (image offset 0)
     const int ng = MF(ng);
-    double g = 0.0, xk = 0.0;
+    double g = 0.0, c0 = 0.0, c1 = 0.0;
 #pragma unroll
-    FOR_S if (CS < ng) { const double c = v[s] / mw[CS]; g += c; xk = (CS == k) ? c : xk; }
-    return wave_sum(xk) / wave_sum(g);
+    FOR_S if (CS < ng) { const double c = v[s] / mw[CS]; g += c; if (s == 0) c0 = c; else c1 = c; }
+    const double ck = (k < 64) ? bcast(c0, k) : bcast(c1, k - 64);   // k uniform: one readlane pair
+    return ck / wave_sum(g);
 }
 // ignition marker after an accepted step to (tn, v): midpoint of the step with the largest dX/dt
 template <int CPL>
 __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int lane, double tn, const double (&v)[CPL]) {
     const double x = uni(mole_frac_of<CPL>(v, lane, a.ign));
-    const double t0 = ud(C->ign_t);
-    const double r = (x - ud(C->ign_x)) / (tn - t0);
-    if (r > ud(C->ign_rate)) { C->ign_rate = r; C->t_ign = 0.5 * (t0 + tn); C->ign_dt = tn - t0; }
+    const double t0 = ud(C->ign_t), xp = ud(C->ign_x), rate = ud(C->ign_rate);
+    const double dt = tn - t0;   // > 0 (accepted step): compare without the division, divide on a new max
+    if (x - xp > rate * dt) {
+        const double r = (x - xp) / dt;
+        if (r > rate) { C->ign_rate = r; C->t_ign = 0.5 * (t0 + tn); C->ign_dt = dt; }
+    }
     C->ign_x = x; C->ign_t = tn;
 }
 // dense output (CVode CV_NORMAL): every tout in (t_{n-1}, t_n] from the Nordsieck array of the step
@@ -628,6 +632,7 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 template <int CPL>
 __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double (&delta)[CPL], int lu_fail) {
     constexpr int VW = 64 * CPL;
+    BR_SUB_T(ps0);
     const CtlArgs a = load_args(C);
     const int n = a.n;
     double ewt[CPL], acor[CPL];
@@ -725,6 +730,8 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
         return A_RHS;
     }
     // ---- cvCompleteStep
+    BR_SUB_ADD(8, ps0);
+    BR_SUB_T(ps1);
     const int nst = ui(C->nst) + 1;
     C->nst = nst;
     const double h = ud(C->h);
@@ -805,6 +812,8 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
 #pragma unroll
     FOR_S z0[s] = V[CS];
     C->eta = eta; C->hprime = hprime; C->qprime = qprime;
+    BR_SUB_ADD(9, ps1);
+    BR_SUB_T(ps2);
     if (a.trace) {
         double yl[CPL];
 #pragma unroll
@@ -845,6 +854,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
         C->eta = hprime / h;
     }
     if (nstloc >= a.max_steps) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
+    BR_SUB_ADD(10, ps2);
     begin_step<CPL>(C, V, lane, a);
     return A_RHS;
 }
@@ -2034,14 +2044,14 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
 }
 
 #if BR_PHASE_CLOCKS
-// diagnostic build only (not declared in brhip.h): read and reset the sub-phase clock sums
+// diagnostic build only (not declared in brhip.h): read and reset the 16 sub-phase clock sums
 // (BR_SUB_ADD slots of brhip_device.hpp)
-extern "C" int br_diag_sub(double* out8) {
-    std::vector<unsigned long long> v((size_t)brhip::SUB_MAXW * 8, 0ull);
+extern "C" int br_diag_sub(double* out16) {
+    std::vector<unsigned long long> v((size_t)brhip::SUB_MAXW * 16, 0ull);
     if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(brhip::g_sub), v.size() * 8) != hipSuccess) return -1;
-    for (int i = 0; i < 8; ++i) out8[i] = 0.0;
+    for (int i = 0; i < 16; ++i) out16[i] = 0.0;
     for (size_t w = 0; w < (size_t)brhip::SUB_MAXW; ++w)
-        for (int i = 0; i < 8; ++i) out8[i] += (double)v[w * 8 + i];
+        for (int i = 0; i < 16; ++i) out16[i] += (double)v[w * 16 + i];
     std::fill(v.begin(), v.end(), 0ull);
     if (hipMemcpyToSymbol(HIP_SYMBOL(brhip::g_sub), v.data(), v.size() * 8) != hipSuccess) return -1;
     return 0;

@@ -153,14 +153,15 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
 // BR_SUB_ADD(slot, t) adds its cycles to g_sub[slot] (one atomic from lane 0); read and reset
 // from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather,
 // 3 ctl_post_rhs, 4..6 gas-only Jacobian: entry loop, column writes, multipliers (+ set passes);
-// 7 begin_step.
+// 7 begin_step; 8..10 ctl_post_solve: convergence + error test, complete + prepare next step,
+// ignition / unstable / tstop checks.
 // ------------------------------------------------------------------------------------
 #if BR_PHASE_CLOCKS
-// one row of 8 sums per resident wave (plain adds by the wave's lane 0: one device-wide atomic
+// one row of 16 sums per resident wave (plain adds by the wave's lane 0: one device-wide atomic
 // counter hit by every wave at every step saturated the memory-side atomic unit and slowed the
 // whole kernel 2x)
 constexpr int SUB_MAXW = 16384;
-__device__ unsigned long long g_sub[SUB_MAXW][8];
+__device__ unsigned long long g_sub[SUB_MAXW][16];
 __device__ __forceinline__ void sub_add(int slot, unsigned long long dt) {
     const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if ((threadIdx.x & 63) == 0 && w < SUB_MAXW) g_sub[w][slot] += dt;
