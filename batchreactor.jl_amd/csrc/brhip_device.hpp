@@ -154,7 +154,7 @@ __device__ __forceinline__ Tab tab_view(const char* base, const DevMech& M) {
 // from the host with br_diag_sub (brhip.hip). Slots: 0 LU panel 1, 1 LU panel 2, 2 LU gather,
 // 3 ctl_post_rhs, 4..6 gas-only Jacobian: entry loop, column writes, multipliers (+ set passes);
 // 7 begin_step; 8..10 ctl_post_solve: convergence + error test, complete + prepare next step,
-// ignition / unstable / tstop checks.
+// ignition / unstable / tstop checks; 11 RHS setup (conc, third-body sums), 12 RHS production.
 // ------------------------------------------------------------------------------------
 #if BR_PHASE_CLOCKS
 // one row of 16 sums per resident wave (plain adds by the wave's lane 0: one device-wide atomic
@@ -558,6 +558,7 @@ __device__ __forceinline__ void rhs(const DevMech& M, const Tab& tb_, const RVie
     typedef Lay<CPL> L;
     const Tab tb = tab_view<CPL>(br_lds, M);
     const RView R = R_;
+    BR_SUB_T(rt0);
     const KPre kp = rx_prefetch(R, lane);
     const int ng = MF(ng), n = MF(n);
     // Y = u/rho, x = (Y/M)/sum(Y/M), p = rho R T / Mbar (:326-338 / :349-353) give the gas
@@ -579,8 +580,11 @@ __device__ __forceinline__ void rhs(const DevMech& M, const Tab& tb_, const RVie
         third_body_sets<CPL>(M, tb, R.sp, Ctot, lane);
     }
     wave_sync();
+    BR_SUB_ADD(11, rt0);
+    BR_SUB_T(rt1);
     production<CPL>(M, tb, R, R_GAS * T, lane, kp);              // :344, :355
     wave_sync();
+    BR_SUB_ADD(12, rt1);
     double w[CPL], sf[CPL];
 #pragma unroll
     for (int s = 0; s < CPL; ++s) {
