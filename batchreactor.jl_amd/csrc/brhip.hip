@@ -97,12 +97,20 @@ enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, aco
 // gas+surface reactor needs 5.7 KB instead of 9.2 KB here (8 reactors per CU instead of 6)
 constexpr int VROW2 = 72;
 __host__ __device__ inline int vec_bytes(int cpl) { return cpl == 2 ? (NVEC * VROW2 + 64) * 8 : NVEC * WAVE * 8; }
-// V[vec * VW + component] accessor (VW = 64 * CPL, the logical row width)
+// Nordsieck / work vectors. BR_VREG = 0: in the reactor's LDS block, V.at(vec, s) = component
+// lane + 64 s of vector vec. BR_VREG = 1: in registers (one double per vector and component slot),
+// stored to the LDS block around each Newton setup (Jacobian + LU, the register peak) and reloaded
+// after it, so the controller's vector updates are register operations instead of LDS round trips.
+#ifndef BR_VREG
+#define BR_VREG 0   // measured: GRI 97.6k vs 98.7k (13 vs 6 spilled VGPRs), surf 171k vs 193k (139 VGPRs: 12 instead of 16 waves/CU), gas+surf +0.3 %
+#endif
 template <int CPL>
-struct VA {
+struct VA {   // LDS rows (VW = 64 * CPL components per vector; CPL = 2 rows are 72 wide, see VROW2)
     typedef __attribute__((address_space(3))) double LD;
     LD* p;
-    __device__ __forceinline__ LD& operator[](int i) const {
+    int lane;
+    __device__ __forceinline__ LD& at(int j, int s) const {
+        const int i = j * 64 * CPL + lane + 64 * s;
         if constexpr (CPL == 1) {
             return p[i];
         } else {
@@ -110,7 +118,46 @@ struct VA {
             return c < VROW2 ? p[row * VROW2 + c] : p[NVEC * VROW2 + (c & 63)];
         }
     }
+    __device__ __forceinline__ void spill() {}
+    __device__ __forceinline__ void reload() {}
 };
+template <int CPL>
+struct VRg {  // registers, backed by the same LDS rows around setups
+    double v[NVEC][CPL];
+    VA<CPL> mem;
+    __device__ __forceinline__ double& at(int j, int s) { return v[j][s]; }
+    __device__ __forceinline__ void spill() {
+#pragma unroll
+        for (int j = 0; j < NVEC; ++j)
+#pragma unroll
+            for (int s = 0; s < CPL; ++s) mem.at(j, s) = v[j][s];
+    }
+    __device__ __forceinline__ void reload() {
+#pragma unroll
+        for (int j = 0; j < NVEC; ++j)
+#pragma unroll
+            for (int s = 0; s < CPL; ++s) v[j][s] = mem.at(j, s);
+    }
+};
+#if BR_VREG
+template <int CPL> using VT = VRg<CPL>;
+#else
+template <int CPL> using VT = VA<CPL>;
+#endif
+// component slot s's value of vector j for a uniform j in [0, QMAX + 1] (register arrays cannot be
+// indexed dynamically: a select chain, scalar branches on the uniform j)
+template <int CPL, class V_>
+__device__ __forceinline__ double vget(V_& V, int j, int s) {
+    double r = 0.0;
+#pragma unroll
+    for (int jj = 0; jj <= QMAX + 1; ++jj) if (jj == j) r = V.at(jj, s);
+    return r;
+}
+template <int CPL, class V_>
+__device__ __forceinline__ void vset(V_& V, int j, int s, double x) {
+#pragma unroll
+    for (int jj = 0; jj <= QMAX + 1; ++jj) if (jj == j) V.at(jj, s) = x;
+}
 typedef __attribute__((address_space(3))) Ctl LCtl;
 typedef __attribute__((address_space(3))) double LDbl;
 
@@ -230,7 +277,7 @@ __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int la
 // dense output (CVode CV_NORMAL): every tout in (t_{n-1}, t_n] from the Nordsieck array of the step
 // just completed, y(t) = sum_j z_j ((t - tn)/h)^j (CVodeGetDky, k = 0)
 template <int CPL>
-__device__ __forceinline__ void dense_output(LCtl* C, VA<CPL> V, const CtlArgs& a, int lane, double tn, double h, int q,
+__device__ __forceinline__ void dense_output(LCtl* C, VT<CPL>& V, const CtlArgs& a, int lane, double tn, double h, int q,
                                              double tlim) {
     constexpr int VW = 64 * CPL;
     int io = ui(C->iout);
@@ -241,8 +288,9 @@ __device__ __forceinline__ void dense_output(LCtl* C, VA<CPL> V, const CtlArgs& 
         double* row = a.yout + ((size_t)a.rid * a.nout + io) * a.n;
 #pragma unroll
         FOR_S {
-            double yv = V[q * VW + CS];
-            for (int j = q - 1; j >= 0; --j) yv = V[j * VW + CS] + sk * yv;
+            double yv = vget<CPL>(V, q, s);
+#pragma unroll
+            for (int j = QMAX - 1; j >= 0; --j) if (j < q) yv = V.at(j, s) + sk * yv;
             if (CS < a.n) row[CS] = yv;
         }
         ++io;
@@ -330,22 +378,25 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
 
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
 template <int CPL>
-__device__ __forceinline__ void cv_rescale(LCtl* C, VA<CPL> V, int lane) {
+__device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     const double eta = ud(C->eta);
     double f = eta;
-    for (int j = 1; j <= q; ++j) {
 #pragma unroll
-        FOR_S V[j * VW + CS] *= f;
-        f *= eta;
+    for (int j = 1; j <= QMAX; ++j) {
+        if (j <= q) {
+#pragma unroll
+            FOR_S V.at(j, s) *= f;
+            f *= eta;
+        }
     }
     const double h = ud(C->hscale) * eta;
     C->h = h; C->hscale = h;
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
 template <int CPL>
-__device__ __forceinline__ void cv_predict(LCtl* C, VA<CPL> V, int lane) {
+__device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     double tn = ud(C->tn) + ud(C->h);
@@ -356,18 +407,18 @@ __device__ __forceinline__ void cv_predict(LCtl* C, VA<CPL> V, int lane) {
     FOR_S {
         double z[QMAX + 1];
 #pragma unroll
-        for (int j = 0; j <= QMAX; ++j) z[j] = V[j * VW + CS];
+        for (int j = 0; j <= QMAX; ++j) z[j] = V.at(j, s);
 #pragma unroll
         for (int k = 1; k <= QMAX; ++k)
 #pragma unroll
             for (int j = QMAX; j >= k; --j)
                 if (j <= q && k <= q) z[j - 1] += z[j];
 #pragma unroll
-        for (int j = 0; j < QMAX; ++j) V[j * VW + CS] = z[j];
+        for (int j = 0; j < QMAX; ++j) V.at(j, s) = z[j];
     }
 }
 template <int CPL>
-__device__ __forceinline__ void cv_restore(LCtl* C, VA<CPL> V, int lane) {
+__device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL>& V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     C->tn = ud(C->saved_t);
@@ -375,19 +426,19 @@ __device__ __forceinline__ void cv_restore(LCtl* C, VA<CPL> V, int lane) {
     FOR_S {
         double z[QMAX + 1];
 #pragma unroll
-        for (int j = 0; j <= QMAX; ++j) z[j] = V[j * VW + CS];
+        for (int j = 0; j <= QMAX; ++j) z[j] = V.at(j, s);
 #pragma unroll
         for (int k = 1; k <= QMAX; ++k)
 #pragma unroll
             for (int j = QMAX; j >= k; --j)
                 if (j <= q && k <= q) z[j - 1] -= z[j];
 #pragma unroll
-        for (int j = 0; j < QMAX; ++j) V[j * VW + CS] = z[j];
+        for (int j = 0; j < QMAX; ++j) V.at(j, s) = z[j];
     }
 }
 // cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
 template <int CPL>
-__device__ __forceinline__ void cv_adjust_order(LCtl* C, VA<CPL> V, int lane, int dq) {
+__device__ __forceinline__ void cv_adjust_order(LCtl* C, VT<CPL>& V, int lane, int dq) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     if (q == 2 && dq != 1) return;
@@ -408,10 +459,10 @@ __device__ __forceinline__ void cv_adjust_order(LCtl* C, VA<CPL> V, int lane, in
         const double A1 = (-alpha0 - alpha1) / prod;
 #pragma unroll
         FOR_S {
-            const double zL = A1 * V[QMAX * VW + CS];
+            const double zL = A1 * V.at(QMAX, s);
 #pragma unroll
-            for (int j = 2; j <= QMAX; ++j) if (j <= q) V[j * VW + CS] += lv[j] * zL;
-            V[(q + 1) * VW + CS] = zL;
+            for (int j = 2; j <= QMAX; ++j) if (j <= q) V.at(j, s) += lv[j] * zL;
+            vset<CPL>(V, q + 1, s, zL);
         }
     } else {
         double hsum = 0.0;
@@ -423,9 +474,9 @@ __device__ __forceinline__ void cv_adjust_order(LCtl* C, VA<CPL> V, int lane, in
         }
 #pragma unroll
         FOR_S {
-            const double zq = V[q * VW + CS];
+            const double zq = vget<CPL>(V, q, s);
 #pragma unroll
-            for (int j = 2; j < QMAX; ++j) if (j < q) V[j * VW + CS] -= lv[j] * zq;
+            for (int j = 2; j < QMAX; ++j) if (j < q) V.at(j, s) -= lv[j] * zq;
         }
     }
 }
@@ -443,7 +494,7 @@ __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, i
 }
 // one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
 template <int CPL>
-__device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL> V, int lane, int nflag) {
+__device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int nflag) {
     constexpr int VW = 64 * CPL;
     cv_predict<CPL>(C, V, lane);
     cv_set(C);
@@ -452,22 +503,22 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL> V, int lane, int 
     C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
                    (nst >= ui(C->nstlp) + MSBP) || (fabs(ud(C->gamrat) - 1.0) > DGMAX);
 #pragma unroll
-    FOR_S V[V_ACOR * VW + CS] = 0.0;
+    FOR_S V.at(V_ACOR, s) = 0.0;
     C->tol = ud(C->tq[4]);
     C->jbad = 0;
     C->jcur_nls = 0;
     C->m_it = 0;
 #pragma unroll
-    FOR_S V[V_Y * VW + CS] = V[CS];   // y = z0
+    FOR_S V.at(V_Y, s) = V.at(0, s);   // y = z0
 }
 template <int CPL>
-__device__ __forceinline__ void begin_step(LCtl* C, VA<CPL> V, int lane, const CtlArgs& a) {
+__device__ __forceinline__ void begin_step(LCtl* C, VT<CPL>& V, int lane, const CtlArgs& a) {
     constexpr int VW = 64 * CPL;
     BR_SUB_T(bt0);
 #pragma unroll
     FOR_S {
-        const double z0 = V[CS];
-        V[V_EWT * VW + CS] = (CS < a.n) ? 1.0 / (a.rtol * fabs(z0) + a.atol) : 1.0;
+        const double z0 = V.at(0, s);
+        V.at(V_EWT, s) = (CS < a.n) ? 1.0 / (a.rtol * fabs(z0) + a.atol) : 1.0;
     }
     C->saved_t = ud(C->tn);
     C->ncf = 0; C->nef = 0;
@@ -487,7 +538,7 @@ __device__ __forceinline__ void begin_step(LCtl* C, VA<CPL> V, int lane, const C
 // Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
 template <int CPL>
-__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
     constexpr int VW = 64 * CPL;
     const CtlArgs a = load_args(C);
     const int n = a.n;
@@ -495,13 +546,13 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
     const int phase = ui(C->phase);
     double z0[CPL];
 #pragma unroll
-    FOR_S z0[s] = V[CS];
+    FOR_S z0[s] = V.at(0, s);
     if (phase == PH_NEWTON) {
         const double rl1 = ud(C->rl1), gamma = ud(C->gamma);
 #pragma unroll
         FOR_S {
-            const double acor = V[V_ACOR * VW + CS];
-            const double delta = (rl1 * V[VW + CS] + acor) - gamma * f[s];   // cvNlsResidual
+            const double acor = V.at(V_ACOR, s);
+            const double delta = (rl1 * V.at(1, s) + acor) - gamma * f[s];   // cvNlsResidual
             rhs_out[s] = -delta;
         }
         if (ui(C->m_it) == 0 && ui(C->callSetup)) {          // cvLsSetup decision
@@ -523,7 +574,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
     if (phase == PH_EF1) {   // restart at order 1 after repeated error-test failures
         const double hh = ud(C->h);
 #pragma unroll
-        FOR_S V[VW + CS] = hh * f[s];
+        FOR_S V.at(1, s) = hh * f[s];
         begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
         C->phase = PH_NEWTON;
         return A_RHS;
@@ -531,8 +582,8 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
     double z1in[CPL], ewt[CPL];
 #pragma unroll
     FOR_S {
-        z1in[s] = (phase == PH_F0) ? f[s] : V[VW + CS];
-        ewt[s] = V[V_EWT * VW + CS];
+        z1in[s] = (phase == PH_F0) ? f[s] : V.at(1, s);
+        ewt[s] = V.at(V_EWT, s);
     }
     if (phase == PH_F0) {
         const double tn = ud(C->tn), tstop = ud(C->tstop);
@@ -542,7 +593,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
         double ratio = 0.0;
 #pragma unroll
         FOR_S {
-            V[VW + CS] = f[s];
+            V.at(1, s) = f[s];
             if (CS < n) ratio = fmax(ratio, fabs(f[s]) / (HUB_FACTOR * fabs(z0[s]) + 1.0 / ewt[s]));
         }
         const double hub_inv = uni(wave_max(ratio));
@@ -555,7 +606,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
         } else {
             C->count1 = 1; C->hnewOK = 0; C->hnew = hg;
 #pragma unroll
-            FOR_S V[V_Y * VW + CS] = hg * f[s] + z0[s];
+            FOR_S V.at(V_Y, s) = hg * f[s] + z0[s];
             C->phase = PH_HIN;
             return A_RHS;
         }
@@ -581,7 +632,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
             C->hg = hg;
             C->count1 = count1 + 1;
 #pragma unroll
-            FOR_S V[V_Y * VW + CS] = hg * z1in[s] + z0[s];
+            FOR_S V.at(V_Y, s) = hg * z1in[s] + z0[s];
             return A_RHS;
         }
         double h0 = H_BIAS * hnew;
@@ -596,7 +647,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL> V, int lane, const do
     C->h = h; C->hscale = h; C->hprime = h;
     trace_row<CPL>(C, a, lane, 0, 0.0, z0, z0);
 #pragma unroll
-    FOR_S V[VW + CS] *= h;
+    FOR_S V.at(1, s) *= h;
     if (a.max_steps <= 0) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
     begin_step<CPL>(C, V, lane, a);
     C->phase = PH_NEWTON;
@@ -630,14 +681,14 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
 template <int CPL>
-__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double (&delta)[CPL], int lu_fail) {
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, double (&delta)[CPL], int lu_fail) {
     constexpr int VW = 64 * CPL;
     BR_SUB_T(ps0);
     const CtlArgs a = load_args(C);
     const int n = a.n;
     double ewt[CPL], acor[CPL];
 #pragma unroll
-    FOR_S ewt[s] = V[V_EWT * VW + CS];
+    FOR_S ewt[s] = V.at(V_EWT, s);
     int nls;                                                   // 0 converged, else failure
     if (lu_fail) {
         nls = 2;
@@ -647,8 +698,8 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
 #pragma unroll
         FOR_S {
             if (gamrat != 1.0) delta[s] *= 2.0 / (1.0 + gamrat);
-            acor[s] = V[V_ACOR * VW + CS] + delta[s];
-            V[V_ACOR * VW + CS] = acor[s];
+            acor[s] = V.at(V_ACOR, s) + delta[s];
+            V.at(V_ACOR, s) = acor[s];
         }
         const double del = wrms_l<CPL>(delta, ewt, lane, n);     // cvNlsConvTest
         const int m = ui(C->m_it);
@@ -668,15 +719,15 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
             }
             if (!fail) {
 #pragma unroll
-                FOR_S V[V_Y * VW + CS] = V[CS] + acor[s];
+                FOR_S V.at(V_Y, s) = V.at(0, s) + acor[s];
                 return A_RHS;
             }
             if (!ui(C->jcur_nls)) {                          // retry with a fresh Jacobian
                 C->callSetup = 1; C->jbad = 1; C->m_it = 0;
 #pragma unroll
                 FOR_S {
-                    V[V_ACOR * VW + CS] = 0.0;
-                    V[V_Y * VW + CS] = V[CS];
+                    V.at(V_ACOR, s) = 0.0;
+                    V.at(V_Y, s) = V.at(0, s);
                 }
                 return A_RHS;
             }
@@ -725,7 +776,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
         const double h = ud(C->h) * ETAMIN;
         C->h = h; C->hscale = h; C->qwait = LONG_WAIT;
 #pragma unroll
-        FOR_S V[V_Y * VW + CS] = V[CS];
+        FOR_S V.at(V_Y, s) = V.at(0, s);
         C->phase = PH_EF1;
         return A_RHS;
     }
@@ -739,19 +790,19 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
     if ((q == 1) && (nst > 1)) C->tau[2] = ud(C->tau[1]);
     C->tau[1] = h;
 #pragma unroll
-    FOR_S acor[s] = V[V_ACOR * VW + CS];
+    FOR_S acor[s] = V.at(V_ACOR, s);
 #pragma unroll
     for (int j = 0; j <= QMAX; ++j) {
         if (j <= q) {
             const double lj = ud(C->l[j]);
 #pragma unroll
-            FOR_S V[j * VW + CS] += lj * acor[s];
+            FOR_S V.at(j, s) += lj * acor[s];
         }
     }
     int qwait = ui(C->qwait) - 1;
     if ((qwait == 1) && (q != QMAX)) {
 #pragma unroll
-        FOR_S V[QMAX * VW + CS] = acor[s];
+        FOR_S V.at(QMAX, s) = acor[s];
         C->saved_tq5 = ud(C->tq[5]);
     }
     // ---- cvPrepareNextStep
@@ -770,7 +821,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
             if (q > 1) {
                 double zq[CPL];
 #pragma unroll
-                FOR_S zq[s] = V[q * VW + CS];
+                FOR_S zq[s] = vget<CPL>(V, q, s);
                 const double ddn = wrms_l<CPL>(zq, ewt, lane, n) * ud(C->tq[1]);
                 etaqm1 = 1.0 / (root_int(BIAS1 * ddn, q) + ADDON);
             }
@@ -779,7 +830,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
                 const double cquot = (ud(C->tq[5]) / saved_tq5) * pow_int(h / ud(C->tau[2]), L);
                 double tempv[CPL];
 #pragma unroll
-                FOR_S tempv[s] = acor[s] - cquot * V[QMAX * VW + CS];
+                FOR_S tempv[s] = acor[s] - cquot * V.at(QMAX, s);
                 const double dup = wrms_l<CPL>(tempv, ewt, lane, n) * ud(C->tq[3]);
                 etaqp1 = 1.0 / (root_int(BIAS3 * dup, L + 1) + ADDON);
             }
@@ -790,7 +841,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
             else {
                 eta = etaqp1; qprime = q + 1;
 #pragma unroll
-                FOR_S V[QMAX * VW + CS] = acor[s];
+                FOR_S V.at(QMAX, s) = acor[s];
             }
         }
         if (eta < THRESH) { eta = 1.0; hprime = h; }                // cvSetEta
@@ -804,20 +855,20 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
     C->etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
     const double tq2 = ud(C->tq[2]);
 #pragma unroll
-    FOR_S V[V_ACOR * VW + CS] = acor[s] * tq2;
+    FOR_S V.at(V_ACOR, s) = acor[s] * tq2;
     const int nstloc = ui(C->nstloc) + 1;
     C->nstloc = nstloc;
     const double tn = ud(C->tn);
     double z0[CPL];
 #pragma unroll
-    FOR_S z0[s] = V[CS];
+    FOR_S z0[s] = V.at(0, s);
     C->eta = eta; C->hprime = hprime; C->qprime = qprime;
     BR_SUB_ADD(9, ps1);
     BR_SUB_T(ps2);
     if (a.trace) {
         double yl[CPL];
 #pragma unroll
-        FOR_S yl[s] = V[V_Y * VW + CS];                     // the last RHS was evaluated at y
+        FOR_S yl[s] = V.at(V_Y, s);                     // the last RHS was evaluated at y
         trace_row<CPL>(C, a, lane, nst, tn, z0, yl);
     }
     if (a.ign >= 0) track_ignition<CPL>(C, a, lane, tn, z0);
@@ -837,9 +888,10 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL> V, int lane, double
         const double sk = (tstop - tn) / h;
 #pragma unroll
         FOR_S {
-            double yv = V[q * VW + CS];
-            for (int j = q - 1; j >= 0; --j) yv = V[j * VW + CS] + sk * yv;
-            V[V_Y * VW + CS] = yv;
+            double yv = vget<CPL>(V, q, s);
+#pragma unroll
+            for (int j = QMAX - 1; j >= 0; --j) if (j < q) yv = V.at(j, s) + sk * yv;
+            V.at(V_Y, s) = yv;
             if (a.trace && nst <= a.trace_cap) {
                 double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + nst) * (2 * n + 4);
                 if (lane == 0 && s == 0) row[0] = tstop;
@@ -925,7 +977,13 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const Tab& tb = W.tb;
     const size_t roff = (size_t)(W.rbase - smem_raw);
     LCtl* C = (LCtl*)(smem_raw + roff);
-    const VA<CPL> V{(LDbl*)(smem_raw + roff + CTL_BYTES)};
+    const VA<CPL> Vm{(LDbl*)(smem_raw + roff + CTL_BYTES), lane};
+#if BR_VREG
+    VT<CPL> V;
+    V.mem = Vm;
+#else
+    VT<CPL> V = Vm;
+#endif
     const RView& S = W.R;
     const int n = M.n;
     const double T = Tv[rid];
@@ -947,10 +1005,10 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         const bool act = CS < n;
         u0[s] = act ? U[(size_t)rid * n + CS] : 0.0;
 #pragma unroll
-        for (int j = 0; j < NVEC; ++j) V[j * VW + CS] = 0.0;
-        V[CS] = u0[s];
-        V[V_Y * VW + CS] = u0[s];
-        V[V_EWT * VW + CS] = act ? 1.0 / (o.rtol * fabs(u0[s]) + o.atol) : 1.0;
+        for (int j = 0; j < NVEC; ++j) V.at(j, s) = 0.0;
+        V.at(0, s) = u0[s];
+        V.at(V_Y, s) = u0[s];
+        V.at(V_EWT, s) = act ? 1.0 / (o.rtol * fabs(u0[s]) + o.atol) : 1.0;
         su += act ? fabs(u0[s]) : 0.0;
     }
 #pragma unroll
@@ -1020,7 +1078,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     for (;;) {
         double y[CPL], f[CPL];
 #pragma unroll
-        FOR_S y[s] = V[V_Y * VW + CS];
+        FOR_S y[s] = V.at(V_Y, s);
         {
             BR_CLK(c0);
             rhs<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, p_last, f);
@@ -1036,6 +1094,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         if (act_code == A_DONE) break;
         int lu_fail = 0;
         if (act_code == A_SETUP) {
+            V.spill();   // (BR_VREG) the vectors wait in LDS while the Jacobian and the LU hold the registers
             if (ui(C->newj)) {
                 BR_CLK(c0);
                 jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
@@ -1046,6 +1105,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
             else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], scr);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
+            V.reload();
         }
         double delta[CPL];
 #pragma unroll
@@ -1069,7 +1129,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const int status = ui(C->status);
 #pragma unroll
     FOR_S {
-        const double u_out = status ? V[CS] : V[V_Y * VW + CS];
+        const double u_out = status ? V.at(0, s) : V.at(V_Y, s);
         if (CS < n) U[(size_t)rid * n + CS] = u_out;
     }
     if (stats && lane == 0) {
