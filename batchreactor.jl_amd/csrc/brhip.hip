@@ -322,12 +322,22 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
             xinv[m] = h / hs;
         }
     }
-    auto xinv_at = [&](int m) {   // uniform m in [2, QMAX + 1]
-        double v = xinv[2];
+    // element m of a small local array for a uniform m: a select chain over opaque copies (written
+    // as a plain chain, the compiler turns it back into a dynamically indexed array in scratch
+    // memory: a global-memory round trip on every cv_set)
+    auto pick = [&](const double* arr, int lo, int hi, int m) {
+        double v = arr[lo];
 #pragma unroll
-        for (int i = 3; i <= QMAX + 1; ++i) v = (m == i) ? xinv[i] : v;
+        for (int i = lo + 1; i <= QMAX + 1; ++i) {
+            if (i <= hi) {
+                double x = arr[i];
+                asm volatile("" : "+v"(x));
+                v = (m == i) ? x : v;
+            }
+        }
         return v;
     };
+    auto xinv_at = [&](int m) { return pick(xinv, 2, QMAX + 1, m); };   // uniform m in [2, QMAX + 1]
     double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0;
     if (q > 1) {
 #pragma unroll
@@ -349,7 +359,7 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
     for (int i = 0; i <= QMAX; ++i) C->l[i] = lv[i];
     const double A1 = 1.0 - alpha0_hat + alpha0;
     const double A2 = 1.0 + q * A1;
-    const double lq = lv[q];
+    const double lq = pick(lv, 1, QMAX, q);
     const double tq2 = fabs(A1 / (alpha0 * A2));
     C->tq[2] = tq2;
     C->tq[5] = fabs(A2 * xistar_inv / (lq * xi_inv));
