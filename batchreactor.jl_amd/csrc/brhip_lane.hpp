@@ -159,11 +159,17 @@ __device__ __forceinline__ double lroot(double x, int L) {
     return (L == 1 || x == 0.0) ? x : y;
 }
 
+// per-lane index tests through an opaque copy of the index: written as plain select chains over a
+// register array, they are turned back into a dynamically indexed array in scratch memory
+__device__ __forceinline__ bool is_idx(int i, int k) {
+    asm volatile("" : "+v"(i));
+    return i == k;
+}
 template <int K>
 __device__ __forceinline__ double sel(const double (&v)[K], int i) {   // v[i], i per lane
     double r = v[0];
 #pragma unroll
-    for (int k = 1; k < K; ++k) r = (i == k) ? v[k] : r;
+    for (int k = 1; k < K; ++k) r = is_idx(i, k) ? v[k] : r;
     return r;
 }
 template <int NM>
@@ -285,7 +291,7 @@ __device__ __forceinline__ void l_adjust_order(LCV& c, ZH<NM>& z, int dq) {
         for (int j = 2; j <= QMAX; ++j) r[j] = z.get(j, i);
         double zq = r[2];
 #pragma unroll
-        for (int j = 3; j <= QMAX; ++j) zq = (q == j) ? r[j] : zq;
+        for (int j = 3; j <= QMAX; ++j) zq = is_idx(q, j) ? r[j] : zq;
         const double src = inc ? A1 * r[QMAX] : zq;
 #pragma unroll
         for (int j = 2; j <= QMAX; ++j) {
@@ -770,9 +776,9 @@ __device__ __forceinline__ void l_getrf_step(double (&a)[NM][NM], unsigned long 
             const double rk = a[k][j];
             double rp = rk;
 #pragma unroll
-            for (int i = k + 1; i < NM; ++i) rp = (p == i) ? a[i][j] : rp;
+            for (int i = k + 1; i < NM; ++i) rp = is_idx(p, i) ? a[i][j] : rp;
 #pragma unroll
-            for (int i = k + 1; i < NM; ++i) a[i][j] = (p == i) ? rk : a[i][j];
+            for (int i = k + 1; i < NM; ++i) a[i][j] = is_idx(p, i) ? rk : a[i][j];
             a[k][j] = rp;
         }
     }
@@ -811,9 +817,9 @@ __device__ __forceinline__ void l_getrs(const GRows& G, const LaneLay& LL, unsig
             const double bk = b[k];
             double bp = bk;
 #pragma unroll
-            for (int i = k + 1; i < NM; ++i) bp = (p == i) ? b[i] : bp;
+            for (int i = k + 1; i < NM; ++i) bp = is_idx(p, i) ? b[i] : bp;
 #pragma unroll
-            for (int i = k + 1; i < NM; ++i) b[i] = (p == i) ? bk : b[i];
+            for (int i = k + 1; i < NM; ++i) b[i] = is_idx(p, i) ? bk : b[i];
             b[k] = bp;
         }
     }
