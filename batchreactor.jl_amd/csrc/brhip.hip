@@ -226,9 +226,11 @@ __device__ __forceinline__ double wrms_l(const double (&v)[CPL], const double (&
 
 struct CtlArgs {   // per-launch constants the controller needs, read (uniform) from the LDS controller
     double rtol, atol, hmax_inv, ufac;
-    double* trace;
-    const double* tout;
-    double* yout;
+    // (global-address-space pointers: generic ones compile to flat accesses, which count on both the
+    // memory and the LDS counter and make the waitcnt pass fall back to full waits after them)
+    BR_GLOBAL double* trace;
+    const BR_GLOBAL double* tout;
+    BR_GLOBAL double* yout;
     int max_steps, trace_cap, rid, n, ign, nout;
 };
 // uniform 64-bit pointer from the LDS controller
@@ -243,9 +245,9 @@ __device__ __forceinline__ P ld_ptr(const __attribute__((address_space(3))) P& f
 __device__ __forceinline__ CtlArgs load_args(LCtl* C) {
     CtlArgs a;
     a.rtol = ud(C->a_rtol); a.atol = ud(C->a_atol); a.hmax_inv = ud(C->a_hmax_inv); a.ufac = ud(C->a_ufac);
-    a.trace = ld_ptr(C->a_trace);
-    a.tout = ld_ptr(C->a_tout);
-    a.yout = ld_ptr(C->a_yout);
+    a.trace = launder(ld_ptr(C->a_trace));
+    a.tout = launder(ld_ptr(C->a_tout));
+    a.yout = launder(ld_ptr(C->a_yout));
     a.max_steps = ui(C->a_max_steps); a.trace_cap = ui(C->a_trace_cap); a.rid = ui(C->a_rid); a.n = ui(C->a_n);
     a.ign = ui(C->a_ign); a.nout = ui(C->a_nout);
     return a;
@@ -285,7 +287,7 @@ __device__ __forceinline__ void dense_output(LCtl* C, VT<CPL>& V, const CtlArgs&
         const double t = uni(a.tout[io]);
         if (!(t <= tlim)) break;
         const double sk = (t - tn) / h;
-        double* row = a.yout + ((size_t)a.rid * a.nout + io) * a.n;
+        auto row = a.yout + ((size_t)a.rid * a.nout + io) * a.n;
 #pragma unroll
         FOR_S {
             double yv = vget<CPL>(V, q, s);
@@ -496,7 +498,7 @@ template <int CPL>
 __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, int step, double t,
                                           const double (&v)[CPL], const double (&y)[CPL]) {
     if (a.trace && step <= a.trace_cap) {
-        double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + step) * (2 * a.n + 4);
+        auto row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + step) * (2 * a.n + 4);
         if (lane == 0) { row[0] = t; row[1] = ud(C->h); row[2] = (double)ui(C->q); row[3] = ud(C->p_last); }
 #pragma unroll
         FOR_S if (CS < a.n) { row[4 + CS] = v[s]; row[4 + a.n + CS] = y[s]; }
@@ -903,7 +905,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
             for (int j = QMAX - 1; j >= 0; --j) if (j < q) yv = V.at(j, s) + sk * yv;
             V.at(V_Y, s) = yv;
             if (a.trace && nst <= a.trace_cap) {
-                double* row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + nst) * (2 * n + 4);
+                auto row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + nst) * (2 * n + 4);
                 if (lane == 0 && s == 0) row[0] = tstop;
                 if (CS < n) row[4 + CS] = yv;
             }
