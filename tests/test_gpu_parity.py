@@ -117,6 +117,28 @@ def test_rhs_and_jacobian_parity(pkg, orc, gpu, case, conv):
         assert np.max(np.abs(J[i] - Jo) / js) < 1e-11, (case, i)
 
 
+@pytest.mark.parametrize("switch", ["BRHIP_JFAST", "BRHIP_SPREAD"])
+def test_jacobian_parity_host_layout_switches(pkg, orc, gpu, monkeypatch, switch):
+    """the A/B layouts behind the host switches (general column-list Jacobian; LDS scatter lists
+    in first-appearance order) stay parity-green on GRI, same bar as the default layout"""
+    monkeypatch.setenv(switch, "0")
+    pm, om = _mechs(pkg, orc, "gri")
+    eng = pkg.Engine(pm)
+    N = 8
+    T, p, x, th = _states(pm, N, 21)
+    Asv = np.ones(N)
+    U = np.stack([pm.initial_state(T[i], p[i], x[i]) for i in range(N)])
+    du = eng.rhs(T, Asv, U)
+    J = eng.jacobian(T, Asv, U)
+    for i in range(N):
+        do, _, _ = om.rhs(T[i], Asv[i], U[i])
+        Jo = om.jac(T[i], Asv[i], U[i])
+        scale = np.abs(Jo).max(1) * np.abs(U[i]).max() + np.abs(do) + 1e-300
+        assert np.all(np.abs(du[i] - do) <= 1e-11 * scale), (switch, i)
+        js = np.abs(Jo).max(1, keepdims=True) + 1e-300
+        assert np.max(np.abs(J[i] - Jo) / js) < 1e-11, (switch, i)
+
+
 def _ignition_inputs(pm, case, N, seed):
     rng = np.random.default_rng(seed)
     if case == "surf":
