@@ -306,7 +306,7 @@ __device__ __forceinline__ double inv_int(int j) {
 }
 
 // cvSet (BDF coefficients l[], tq[], gamma) for the current q, h, tau
-__device__ __forceinline__ void cv_set(LCtl* C) {
+__device__ __forceinline__ void cv_set(LCtl* C, double& tq4_out, double& gamrat_out) {
     const int q = ui(C->q), qwait = ui(C->qwait), nst = ui(C->nst);
     const double h = ud(C->h);
     double lv[QMAX + 1] = {1.0, 1.0, 0.0, 0.0, 0.0, 0.0};
@@ -379,13 +379,15 @@ __device__ __forceinline__ void cv_set(LCtl* C) {
         const double Cppinv = (1.0 - A6 + A5) / A2;
         C->tq[3] = fabs(Cppinv / (xi_inv * (q + 2) * A5));
     }
-    C->tq[4] = CORTES / tq2;
+    tq4_out = CORTES / tq2;
+    C->tq[4] = tq4_out;
     const double rl1 = 1.0 / lv[1];
     C->rl1 = rl1;
     const double gamma = h * rl1;
     C->gamma = gamma;
     if (nst == 0) C->gammap = gamma;
-    C->gamrat = (nst > 0) ? gamma / ud(C->gammap) : 1.0;
+    gamrat_out = (nst > 0) ? gamma / ud(C->gammap) : 1.0;
+    C->gamrat = gamrat_out;
 }
 
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
@@ -393,7 +395,7 @@ template <int CPL>
 __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
     constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
-    const double eta = ud(C->eta);
+    const double eta = ud(C->eta), hscale = ud(C->hscale);
     double f = eta;
 #pragma unroll
     for (int j = 1; j <= QMAX; ++j) {
@@ -403,7 +405,7 @@ __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
             f *= eta;
         }
     }
-    const double h = ud(C->hscale) * eta;
+    const double h = hscale * eta;
     C->h = h; C->hscale = h;
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
@@ -509,14 +511,15 @@ template <int CPL>
 __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int nflag) {
     constexpr int VW = 64 * CPL;
     cv_predict<CPL>(C, V, lane);
-    cv_set(C);
+    double tq4, gamrat;
+    cv_set(C, tq4, gamrat);
     const int nst = ui(C->nst);
     C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
     C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
-                   (nst >= ui(C->nstlp) + MSBP) || (fabs(ud(C->gamrat) - 1.0) > DGMAX);
+                   (nst >= ui(C->nstlp) + MSBP) || (fabs(gamrat - 1.0) > DGMAX);
 #pragma unroll
     FOR_S V.at(V_ACOR, s) = 0.0;
-    C->tol = ud(C->tq[4]);
+    C->tol = tq4;
     C->jbad = 0;
     C->jcur_nls = 0;
     C->m_it = 0;
@@ -527,15 +530,16 @@ template <int CPL>
 __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL>& V, int lane, const CtlArgs& a) {
     constexpr int VW = 64 * CPL;
     BR_SUB_T(bt0);
+    const double tn = ud(C->tn), hprime = ud(C->hprime), h = ud(C->h);   // read before the V stores
+    const int nst = ui(C->nst), qp = ui(C->qprime), q = ui(C->q);
 #pragma unroll
     FOR_S {
         const double z0 = V.at(0, s);
         V.at(V_EWT, s) = (CS < a.n) ? 1.0 / (a.rtol * fabs(z0) + a.atol) : 1.0;
     }
-    C->saved_t = ud(C->tn);
+    C->saved_t = tn;
     C->ncf = 0; C->nef = 0;
-    if ((ui(C->nst) > 0) && (ud(C->hprime) != ud(C->h))) {
-        const int qp = ui(C->qprime), q = ui(C->q);
+    if ((nst > 0) && (hprime != h)) {
         if (qp != q) {
             cv_adjust_order<CPL>(C, V, lane, qp - q);
             C->q = qp; C->L = qp + 1; C->qwait = qp + 1;
@@ -795,36 +799,51 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     // ---- cvCompleteStep
     BR_SUB_ADD(8, ps0);
     BR_SUB_T(ps1);
+    // every controller scalar this part reads, loaded in one batch before the first Nordsieck store
+    // (V shares LDS with the controller, so a load placed after a V store cannot be hoisted above
+    // it: read in place, each one was its own LDS round trip)
     const int nst = ui(C->nst) + 1;
-    C->nst = nst;
     const double h = ud(C->h);
-    for (int i = q; i >= 2; --i) C->tau[i] = ud(C->tau[i - 1]);
-    if ((q == 1) && (nst > 1)) C->tau[2] = ud(C->tau[1]);
+    double tauv[QMAX + 1], lv[QMAX + 1];
+#pragma unroll
+    for (int i = 1; i <= QMAX; ++i) tauv[i] = ud(C->tau[i]);
+#pragma unroll
+    for (int j = 0; j <= QMAX; ++j) lv[j] = ud(C->l[j]);
+    int qwait = ui(C->qwait) - 1;
+    const double etamax = ud(C->etamax), tq1 = ud(C->tq[1]), tq2 = ud(C->tq[2]), tq3 = ud(C->tq[3]);
+    const double tq5 = ud(C->tq[5]);
+    double saved_tq5 = ud(C->saved_tq5);
+    const int L = ui(C->L);
+    const int nstloc = ui(C->nstloc) + 1;
+    const double tn = ud(C->tn), tstop = ud(C->tstop), ulimit = ud(C->ulimit);
+    C->nst = nst;
+    double tau2 = tauv[2];   // tau[2] after the shift
+#pragma unroll
+    for (int i = QMAX; i >= 2; --i) if (i <= q) C->tau[i] = tauv[i - 1];
+    if (q >= 2 || nst > 1) tau2 = tauv[1];
+    if ((q == 1) && (nst > 1)) C->tau[2] = tauv[1];
     C->tau[1] = h;
 #pragma unroll
     FOR_S acor[s] = V.at(V_ACOR, s);
 #pragma unroll
     for (int j = 0; j <= QMAX; ++j) {
         if (j <= q) {
-            const double lj = ud(C->l[j]);
 #pragma unroll
-            FOR_S V.at(j, s) += lj * acor[s];
+            FOR_S V.at(j, s) += lv[j] * acor[s];
         }
     }
-    int qwait = ui(C->qwait) - 1;
     if ((qwait == 1) && (q != QMAX)) {
 #pragma unroll
         FOR_S V.at(QMAX, s) = acor[s];
-        C->saved_tq5 = ud(C->tq[5]);
+        saved_tq5 = tq5;
+        C->saved_tq5 = tq5;
     }
     // ---- cvPrepareNextStep
     double eta = 1.0, hprime = h;
     int qprime = q;
-    const double etamax = ud(C->etamax);
     if (etamax == 1.0) {
         qwait = qwait > 2 ? qwait : 2;
     } else {
-        const int L = ui(C->L);
         const double etaq = 1.0 / (root_int(BIAS2 * dsm, L) + ADDON);
         if (qwait != 0) { eta = etaq; }
         else {
@@ -834,16 +853,15 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
                 double zq[CPL];
 #pragma unroll
                 FOR_S zq[s] = vget<CPL>(V, q, s);
-                const double ddn = wrms_l<CPL>(zq, ewt, lane, n) * ud(C->tq[1]);
+                const double ddn = wrms_l<CPL>(zq, ewt, lane, n) * tq1;
                 etaqm1 = 1.0 / (root_int(BIAS1 * ddn, q) + ADDON);
             }
-            const double saved_tq5 = ud(C->saved_tq5);
             if (q != QMAX && saved_tq5 != 0.0) {
-                const double cquot = (ud(C->tq[5]) / saved_tq5) * pow_int(h / ud(C->tau[2]), L);
+                const double cquot = (tq5 / saved_tq5) * pow_int(h / tau2, L);
                 double tempv[CPL];
 #pragma unroll
                 FOR_S tempv[s] = acor[s] - cquot * V.at(QMAX, s);
-                const double dup = wrms_l<CPL>(tempv, ewt, lane, n) * ud(C->tq[3]);
+                const double dup = wrms_l<CPL>(tempv, ewt, lane, n) * tq3;
                 etaqp1 = 1.0 / (root_int(BIAS3 * dup, L + 1) + ADDON);
             }
             const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
@@ -865,12 +883,9 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     }
     C->qwait = qwait;
     C->etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-    const double tq2 = ud(C->tq[2]);
 #pragma unroll
     FOR_S V.at(V_ACOR, s) = acor[s] * tq2;
-    const int nstloc = ui(C->nstloc) + 1;
     C->nstloc = nstloc;
-    const double tn = ud(C->tn);
     double z0[CPL];
 #pragma unroll
     FOR_S z0[s] = V.at(0, s);
@@ -890,10 +905,9 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
 #pragma unroll
         FOR_S if (CS < n) { const double a = fabs(z0[s]); zm = fmax(zm, a == a ? a : INFINITY); }
         const double mx = uni(wave_max(zm));
-        if (!(mx < INFINITY) || mx > ud(C->ulimit)) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
+        if (!(mx < INFINITY) || mx > ulimit) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
     }
     // CVode ONE_STEP + tstop handling
-    const double tstop = ud(C->tstop);
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
     if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
         if (a.nout) dense_output<CPL>(C, V, a, lane, tn, h, q, tstop);
