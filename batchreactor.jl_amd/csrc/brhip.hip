@@ -706,11 +706,16 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
 #pragma unroll
     FOR_S ewt[s] = V.at(V_EWT, s);
     int nls;                                                   // 0 converged, else failure
+    double acnrm = 0.0;
+    const double tq2_e = ud(C->tq[2]);
     if (lu_fail) {
         nls = 2;
     } else {
         C->nni = ui(C->nni) + 1;
         const double gamrat = ud(C->gamrat);
+        const int m = ui(C->m_it);                            // read before the V stores
+        double crate = ud(C->crate);
+        const double delp = ud(C->delp), tol = ud(C->tol);
 #pragma unroll
         FOR_S {
             if (gamrat != 1.0) delta[s] *= 2.0 / (1.0 + gamrat);
@@ -718,13 +723,11 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
             V.at(V_ACOR, s) = acor[s];
         }
         const double del = wrms_l<CPL>(delta, ewt, lane, n);     // cvNlsConvTest
-        const int m = ui(C->m_it);
-        double crate = ud(C->crate);
-        const double delp = ud(C->delp);
         if (m > 0) { crate = fmax(CRDOWN * crate, del / delp); C->crate = crate; }
-        const double dcon = del * fmin(1.0, crate) / ud(C->tol);
+        const double dcon = del * fmin(1.0, crate) / tol;
         if (dcon <= 1.0) {
-            C->acnrm = (m == 0) ? del : wrms_l<CPL>(acor, ewt, lane, n);
+            acnrm = (m == 0) ? del : wrms_l<CPL>(acor, ewt, lane, n);
+            C->acnrm = acnrm;
             nls = 0;
         } else {
             bool fail = (m >= 1) && (del > RDIV * delp);
@@ -763,7 +766,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
         return A_RHS;
     }
     // ---- cvDoErrorTest
-    const double dsm = ud(C->acnrm) * ud(C->tq[2]);
+    const double dsm = acnrm * tq2_e;
     const int q = ui(C->q);
     if (dsm > 1.0) {
         const int nef = ui(C->nef) + 1;
