@@ -305,14 +305,29 @@ __device__ __forceinline__ double inv_int(int j) {
     return j == 1 ? 1.0 : j == 2 ? 0.5 : j == 3 ? 1.0 / 3.0 : j == 4 ? 0.25 : j == 5 ? 0.2 : j == 6 ? 1.0 / 6.0 : 1.0 / j;
 }
 
+// the controller scalars one attempt (predict + cvSet) reads, loaded in one batch before the
+// prediction's Nordsieck stores (V shares LDS with the controller: a load after a V store waits)
+struct AttemptIn {
+    int q, qwait, nst, nstlp;
+    double h, tn, tstop, gammap;
+    double tau[QMAX + 2];
+};
+__device__ __forceinline__ AttemptIn load_attempt(LCtl* C) {
+    AttemptIn in;
+    in.q = ui(C->q); in.qwait = ui(C->qwait); in.nst = ui(C->nst); in.nstlp = ui(C->nstlp);
+    in.h = ud(C->h); in.tn = ud(C->tn); in.tstop = ud(C->tstop); in.gammap = ud(C->gammap);
+#pragma unroll
+    for (int i = 0; i < QMAX + 2; ++i) in.tau[i] = ud(C->tau[i]);
+    return in;
+}
 // cvSet (BDF coefficients l[], tq[], gamma) for the current q, h, tau
-__device__ __forceinline__ void cv_set(LCtl* C, double& tq4_out, double& gamrat_out) {
-    const int q = ui(C->q), qwait = ui(C->qwait), nst = ui(C->nst);
-    const double h = ud(C->h);
+__device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4_out, double& gamrat_out) {
+    const int q = in.q, qwait = in.qwait, nst = in.nst;
+    const double h = in.h;
     double lv[QMAX + 1] = {1.0, 1.0, 0.0, 0.0, 0.0, 0.0};
     double tau[QMAX + 2];
 #pragma unroll
-    for (int i = 0; i < QMAX + 2; ++i) tau[i] = ud(C->tau[i]);
+    for (int i = 0; i < QMAX + 2; ++i) tau[i] = in.tau[i];
     // h / hsum_m for every m up front (hsum_m = h + tau[1] + ... + tau[m-1], summed in CVODE's
     // order): the divisions are independent, so they overlap instead of forming a chain
     double xinv[QMAX + 2];
@@ -386,7 +401,7 @@ __device__ __forceinline__ void cv_set(LCtl* C, double& tq4_out, double& gamrat_
     const double gamma = h * rl1;
     C->gamma = gamma;
     if (nst == 0) C->gammap = gamma;
-    gamrat_out = (nst > 0) ? gamma / ud(C->gammap) : 1.0;
+    gamrat_out = (nst > 0) ? gamma / in.gammap : 1.0;
     C->gamrat = gamrat_out;
 }
 
@@ -410,12 +425,12 @@ __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
 template <int CPL>
-__device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane) {
+__device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane, const AttemptIn& in) {
     constexpr int VW = 64 * CPL;
-    const int q = ui(C->q);
-    double tn = ud(C->tn) + ud(C->h);
-    const double tstop = ud(C->tstop);
-    if ((tn - tstop) * ud(C->h) > 0) tn = tstop;
+    const int q = in.q;
+    double tn = in.tn + in.h;
+    const double tstop = in.tstop;
+    if ((tn - tstop) * in.h > 0) tn = tstop;
     C->tn = tn;
 #pragma unroll
     FOR_S {
@@ -510,13 +525,14 @@ __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, i
 template <int CPL>
 __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int nflag) {
     constexpr int VW = 64 * CPL;
-    cv_predict<CPL>(C, V, lane);
+    const AttemptIn in = load_attempt(C);
+    cv_predict<CPL>(C, V, lane, in);
     double tq4, gamrat;
-    cv_set(C, tq4, gamrat);
-    const int nst = ui(C->nst);
+    cv_set(C, in, tq4, gamrat);
+    const int nst = in.nst;
     C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
     C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
-                   (nst >= ui(C->nstlp) + MSBP) || (fabs(gamrat - 1.0) > DGMAX);
+                   (nst >= in.nstlp + MSBP) || (fabs(gamrat - 1.0) > DGMAX);
 #pragma unroll
     FOR_S V.at(V_ACOR, s) = 0.0;
     C->tol = tq4;
