@@ -97,13 +97,9 @@ enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, aco
 // gas+surface reactor needs 5.7 KB instead of 9.2 KB here (8 reactors per CU instead of 6)
 constexpr int VROW2 = 72;
 __host__ __device__ inline int vec_bytes(int cpl) { return cpl == 2 ? (NVEC * VROW2 + 64) * 8 : NVEC * WAVE * 8; }
-// Nordsieck / work vectors. BR_VREG = 0: in the reactor's LDS block, V.at(vec, s) = component
-// lane + 64 s of vector vec. BR_VREG = 1: in registers (one double per vector and component slot),
-// stored to the LDS block around each Newton setup (Jacobian + LU, the register peak) and reloaded
-// after it, so the controller's vector updates are register operations instead of LDS round trips.
-#ifndef BR_VREG
-#define BR_VREG 0   // measured: GRI 97.6k vs 98.7k (13 vs 6 spilled VGPRs), surf 171k vs 193k (139 VGPRs: 12 instead of 16 waves/CU), gas+surf +0.3 %
-#endif
+// Nordsieck / work vectors in the reactor's LDS block: V.at(vec, s) = component lane + 64 s of
+// vector vec. (Register-resident vectors stored to LDS around each Newton setup measured GRI
+// -1.1 %, surf -11 % in round 2: the extra VGPRs cost occupancy.)
 template <int CPL>
 struct VA {   // LDS rows (VW = 64 * CPL components per vector; CPL = 2 rows are 72 wide, see VROW2)
     typedef __attribute__((address_space(3))) double LD;
@@ -118,32 +114,8 @@ struct VA {   // LDS rows (VW = 64 * CPL components per vector; CPL = 2 rows are
             return c < VROW2 ? p[row * VROW2 + c] : p[NVEC * VROW2 + (c & 63)];
         }
     }
-    __device__ __forceinline__ void spill() {}
-    __device__ __forceinline__ void reload() {}
 };
-template <int CPL>
-struct VRg {  // registers, backed by the same LDS rows around setups
-    double v[NVEC][CPL];
-    VA<CPL> mem;
-    __device__ __forceinline__ double& at(int j, int s) { return v[j][s]; }
-    __device__ __forceinline__ void spill() {
-#pragma unroll
-        for (int j = 0; j < NVEC; ++j)
-#pragma unroll
-            for (int s = 0; s < CPL; ++s) mem.at(j, s) = v[j][s];
-    }
-    __device__ __forceinline__ void reload() {
-#pragma unroll
-        for (int j = 0; j < NVEC; ++j)
-#pragma unroll
-            for (int s = 0; s < CPL; ++s) v[j][s] = mem.at(j, s);
-    }
-};
-#if BR_VREG
-template <int CPL> using VT = VRg<CPL>;
-#else
 template <int CPL> using VT = VA<CPL>;
-#endif
 // component slot s's value of vector j for a uniform j in [0, QMAX + 1] (register arrays cannot be
 // indexed dynamically: a select chain, scalar branches on the uniform j)
 template <int CPL, class V_>
@@ -281,7 +253,6 @@ __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int la
 template <int CPL>
 __device__ __forceinline__ void dense_output(LCtl* C, VT<CPL>& V, const CtlArgs& a, int lane, double tn, double h, int q,
                                              double tlim) {
-    constexpr int VW = 64 * CPL;
     int io = ui(C->iout);
     while (io < a.nout) {
         const double t = uni(a.tout[io]);
@@ -408,7 +379,6 @@ __device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
 template <int CPL>
 __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
-    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     const double eta = ud(C->eta), hscale = ud(C->hscale);
     double f = eta;
@@ -426,7 +396,6 @@ __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
 // prediction (tn += h, Pascal triangle on z) and its inverse
 template <int CPL>
 __device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane, const AttemptIn& in) {
-    constexpr int VW = 64 * CPL;
     const int q = in.q;
     double tn = in.tn + in.h;
     const double tstop = in.tstop;
@@ -448,7 +417,6 @@ __device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane, const 
 }
 template <int CPL>
 __device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL>& V, int lane) {
-    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     C->tn = ud(C->saved_t);
 #pragma unroll
@@ -468,7 +436,6 @@ __device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL>& V, int lane) {
 // cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
 template <int CPL>
 __device__ __forceinline__ void cv_adjust_order(LCtl* C, VT<CPL>& V, int lane, int dq) {
-    constexpr int VW = 64 * CPL;
     const int q = ui(C->q);
     if (q == 2 && dq != 1) return;
     double lv[QMAX + 1] = {0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
@@ -524,7 +491,6 @@ __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, i
 // one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
 template <int CPL>
 __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int nflag) {
-    constexpr int VW = 64 * CPL;
     const AttemptIn in = load_attempt(C);
     cv_predict<CPL>(C, V, lane, in);
     double tq4, gamrat;
@@ -544,7 +510,6 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int
 }
 template <int CPL>
 __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL>& V, int lane, const CtlArgs& a) {
-    constexpr int VW = 64 * CPL;
     BR_SUB_T(bt0);
     const double tn = ud(C->tn), hprime = ud(C->hprime), h = ud(C->h);   // read before the V stores
     const int nst = ui(C->nst), qp = ui(C->qprime), q = ui(C->q);
@@ -571,7 +536,6 @@ __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL>& V, int lane, const 
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
 template <int CPL>
 __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
-    constexpr int VW = 64 * CPL;
     const CtlArgs a = load_args(C);
     const int n = a.n;
     C->nfe = ui(C->nfe) + 1;
@@ -714,7 +678,6 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
 template <int CPL>
 __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, double (&delta)[CPL], int lu_fail) {
-    constexpr int VW = 64 * CPL;
     BR_SUB_T(ps0);
     const CtlArgs a = load_args(C);
     const int n = a.n;
@@ -911,6 +874,14 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     C->eta = eta; C->hprime = hprime; C->qprime = qprime;
     BR_SUB_ADD(9, ps1);
     BR_SUB_T(ps2);
+    {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor);
+        // first, as in the oracle: an unstable step writes no trace row and no dense output
+        double zm = 0.0;
+#pragma unroll
+        FOR_S if (CS < n) { const double a = fabs(z0[s]); zm = fmax(zm, a == a ? a : INFINITY); }
+        const double mx = uni(wave_max(zm));
+        if (!(mx < INFINITY) || mx > ulimit) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
+    }
     if (a.trace) {
         double yl[CPL];
 #pragma unroll
@@ -919,13 +890,6 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     }
     if (a.ign >= 0) track_ignition<CPL>(C, a, lane, tn, z0);
     if (a.nout) dense_output<CPL>(C, V, a, lane, tn, h, q, tn);
-    {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor)
-        double zm = 0.0;
-#pragma unroll
-        FOR_S if (CS < n) { const double a = fabs(z0[s]); zm = fmax(zm, a == a ? a : INFINITY); }
-        const double mx = uni(wave_max(zm));
-        if (!(mx < INFINITY) || mx > ulimit) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
-    }
     // CVode ONE_STEP + tstop handling
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
     if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
@@ -963,9 +927,6 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
 // ------------------------------------------------------------------------------------
 #ifndef BR_WPE
 #define BR_WPE 2
-#endif
-#ifndef BR_ACC_NMAX
-#define BR_ACC_NMAX 0   // largest NMAX whose LU factors live in AGPRs (0: all in global memory)
 #endif
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
@@ -1023,12 +984,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const size_t roff = (size_t)(W.rbase - smem_raw);
     LCtl* C = (LCtl*)(smem_raw + roff);
     const VA<CPL> Vm{(LDbl*)(smem_raw + roff + CTL_BYTES), lane};
-#if BR_VREG
-    VT<CPL> V;
-    V.mem = Vm;
-#else
     VT<CPL> V = Vm;
-#endif
     const RView& S = W.R;
     const int n = M.n;
     const double T = Tv[rid];
@@ -1081,6 +1037,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     if (o.rid_t0 && stats) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) st_in[k] = uni(stats[(size_t)rid * BR_NSTAT + k]);
+        // the step limit is on the whole run (SciML maxiters): the lane pass's steps count against it
+        C->a_max_steps = max(o.max_steps - (int)st_in[0], 0);
         if (o.ign >= 0) {
             C->ign_rate = uni(stats[(size_t)rid * BR_NSTAT + 17]);
             C->t_ign = uni(stats[(size_t)rid * BR_NSTAT + 16]);
@@ -1114,11 +1072,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     int perm[CPL];
 #pragma unroll
     FOR_S perm[s] = CS;
-    // LU factors resident in AGPRs across the Newton iterations that reuse them (CPL = 1, NMAX <=
-    // BR_ACC_NMAX); otherwise in the per-slot global workspace
-    constexpr bool ACCF = (CPL == 1) && (NMAX <= BR_ACC_NMAX);
-    AccFac<ACCF ? NMAX : 1> af;
-    LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // LU scratch (pivot-row buffer): the production sums are idle then
+    LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // solve / LU scratch: the production sums are idle then
     double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
     for (;;) {
         double y[CPL], f[CPL];
@@ -1139,26 +1093,22 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         if (act_code == A_DONE) break;
         int lu_fail = 0;
         if (act_code == A_SETUP) {
-            V.spill();   // (BR_VREG) the vectors wait in LDS while the Jacobian and the LU hold the registers
             if (ui(C->newj)) {
                 BR_CLK(c0);
                 jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            if constexpr (ACCF) lu_fail = lu_factor<NMAX, true>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], scr, &af);
-            else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0], scr);
+            if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
-            V.reload();
         }
         double delta[CPL];
 #pragma unroll
         FOR_S delta[s] = 0.0;
         if (!lu_fail) {
             BR_CLK(c0);
-            if constexpr (ACCF) delta[0] = lu_solve_acc<NMAX>(af, n, lane, perm[0], b[0]);
-            else if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
+            if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
             else {
                 lu_solve2<NMAX>(LUsave, scr, n, lane, perm, b);
                 delta[0] = b[0];
@@ -1636,13 +1586,9 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         for (int k = 0; k < ng; ++k) mw[k] = d->molwt[k];
         for (int i = 0; i < ns; ++i) mw[SPW + ng + i] = d->sigma ? d->sigma[i] : 1.0;
         if (nrg) {
-#if BR_RX_SPLIT
             uint32_t* ra = reinterpret_cast<uint32_t*>(img.data() + IMG_RX_OFF);
             for (int i = 0; i < nrg; ++i)
                 for (int w = 0; w < RX_WORDS; ++w) ra[(w < 4 ? 4 * i : 4 * nrg + 4 * i) + (w & 3)] = rx[(size_t)RX_WORDS * i + w];
-#else
-            memcpy(img.data() + IMG_RX_OFF, rx.data(), rx.size() * 4);
-#endif
         }
         if (nrs) memcpy(img.data() + M.sx_off, sx.data(), sx.size() * 4);
         if (nrs) memcpy(img.data() + M.sxe_off, sxe.data(), sxe.size() * 8);
@@ -2085,7 +2031,7 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     int perm = lane;
-    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm, (LDSd*)prow);
+    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0, (LDSd*)prow);

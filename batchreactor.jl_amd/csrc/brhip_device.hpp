@@ -72,12 +72,9 @@ __device__ __forceinline__ T karg_field(size_t off) {
     return *(cT*)(p + off);
 }
 #define MF(f) (::brhip::karg_field<decltype(::brhip::DevMech::f)>(offsetof(::brhip::DevMech, f)))
-// RX records in the image: split (BR_RX_SPLIT = 1) into words 0..3 of every reaction, then words
-// 4..7 (two arrays with a 16-byte stride: the b128 record reads of 64 consecutive reactions hit
-// every LDS bank once; with the 32-byte stride of whole records two lanes share each bank)
-#ifndef BR_RX_SPLIT
-#define BR_RX_SPLIT 1
-#endif
+// RX records in the image: split into words 0..3 of every reaction, then words 4..7 (two arrays
+// with a 16-byte stride: the b128 record reads of 64 consecutive reactions hit every LDS bank
+// once; with the 32-byte stride of whole records two lanes share each bank)
 template <class P>
 struct RxRec {
     P a, b;
@@ -85,11 +82,7 @@ struct RxRec {
 };
 template <class P>
 __device__ __forceinline__ RxRec<P> rx_rec(P rx, int r) {
-#if BR_RX_SPLIT
     return {rx + 4 * r, rx + 4 * MF(nrg) + 4 * r};
-#else
-    return {rx + 8 * r, rx + 8 * r + 4};
-#endif
 }
 
 // RX record: w0 reactant species (4 x 8 bit; pad = SP_ONE, a slot holding 1.0, so the
@@ -194,36 +187,12 @@ __device__ __forceinline__ double bcast(double v, int lane) {
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-// broadcast through the LDS crossbar (ds_bpermute, no LDS memory): runs on the LDS pipe, so a
-// stream of independent broadcasts (the LU's pivot-row elements) costs no VALU issue slots
-__device__ __forceinline__ double bcast_x(double v, int lane_addr4) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(lane_addr4, (int)(b & 0xffffffffLL));
-    const int hi = __builtin_amdgcn_ds_bpermute(lane_addr4, (int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-// broadcast of a pivot-row element in the LU: through the LDS crossbar (BR_LU_XBAR = 1: two
-// ds_bpermute on the LDS pipe, no VALU issue; the kernel is VALU-issue-bound) or v_readlane
-#ifndef BR_LU_XBAR
-#define BR_LU_XBAR 0   // measured: GRI 78.2k vs 90.8k, gas+surf 16.8k vs 17.8k reactors/s (the bpermute latency sits on the elimination chain)
-#endif
-__device__ __forceinline__ double bcast_lu(double v, int p) {
-#if BR_LU_XBAR
-    return bcast_x(v, p * 4);
-#else
-    return bcast(v, p);
-#endif
-}
-// uniform fp64 values: v_readfirstlane into SGPRs (BR_UNI_D = 1) or left in VGPRs (0). fp64
-// arithmetic and compares run on the VALU either way, so the two readfirstlanes buy only SGPR
-// residency and scalar branches
-#ifndef BR_UNI_D
-#define BR_UNI_D 1
-#endif
+// broadcast of a pivot-row element in the LU (a v_readlane pair; the LDS-crossbar form measured
+// 78.2k vs 90.8k GRI reactors/s in round 2: its latency sits on the elimination chain)
+__device__ __forceinline__ double bcast_lu(double v, int p) { return bcast(v, p); }
+// uniform fp64 values: v_readfirstlane into SGPRs (scalar residency and scalar branches; fp64
+// arithmetic and compares still run on the VALU)
 __device__ __forceinline__ double uni(double v) {
-#if !BR_UNI_D
-    return v;
-#endif
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
     const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
@@ -1029,6 +998,9 @@ __device__ __forceinline__ int pivot_lane(double v, bool cand) {   // v = |a_ik|
 // s > k, U'[s][k] = (D^-1 U)[s][k] on rows s < k and 0 on s = k; then D^-1 in step order.
 // The forward sweep reads only rows below the diagonal and the backward sweep only rows above
 // it (exec-masked loads skip whole 128-B lines), so a solve moves ~n^2 doubles instead of 2*n*64.
+// (A packed-triangle layout -- each sweep reading one triangle front to back, 25.5 KB instead of
+// ~29 KB per GRI solve from the fabric -- measured 2.7 % slower in round 3: its column segments
+// start at arbitrary 8-B offsets, so every load instruction spans one more 128-B line.)
 struct LUWs {
     BR_GLOBAL double* M;
     BR_GLOBAL double* D;
@@ -1036,58 +1008,14 @@ struct LUWs {
 typedef __attribute__((address_space(3))) double LDSd;
 typedef __attribute__((address_space(3))) int LDSi;
 
-// Pivot-row broadcast through LDS (BR_LU_LDSB = 1, off by default): per elimination step the pivot lane writes its
-// live row segment to a 64-double LDS row buffer (ds_write_b128 from one lane) and every lane reads
-// it back as broadcast ds_read_b128, so the rank-1 update costs one VALU FMA per element instead of
-// two v_readlane_b32 + FMA (at 4 waves/SIMD the integrator is VALU-issue-bound).
-#ifndef BR_LU_LDSB
-#define BR_LU_LDSB 0   // measured: GRI 75.8k vs 85.2k, surf 156k vs 174k reactors/s (the LDS round trip sits on the elimination chain)
-#endif
-template <int W>
-__device__ __forceinline__ void prow_put(LDSd* pr, const double (&a)[W], int off, int live) {
-    // pr[j] = a[j + off] for the chunks j < live (off = 1: the shifted right-looking segment)
-#pragma unroll
-    for (int c = 0; c < W; c += 8) {
-        if (c < live) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) pr[c + i] = (c + i + off < W) ? a[c + i + off] : 0.0;
-        }
-    }
-}
-
-// AGPR-resident factors (CPL = 1): after lu_factor's final gather, lane s holds row s (pivot-step
-// order) of the combined factor matrix and D^-1 in accumulation registers. They stay there
-// across the Newton iterations that reuse them, so a solve reads no memory (the global
-// workspace copy is never written). Every def and use is an inline-asm operand with the "a"
-// constraint, so the register allocator keeps the values in AGPRs (2 x 32-bit per double);
-// all indices are compile-time (unrolled loops), so no dynamic register indexing.
-template <int NMAX>
-struct AccFac {
-    unsigned lo[NMAX], hi[NMAX];
-    unsigned dlo, dhi;
-};
-__device__ __forceinline__ void acc_put(unsigned& alo, unsigned& ahi, double v) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    asm("v_accvgpr_write_b32 %0, %1" : "=a"(alo) : "v"((unsigned)b));
-    asm("v_accvgpr_write_b32 %0, %1" : "=a"(ahi) : "v"((unsigned)(b >> 32)));
-}
-__device__ __forceinline__ double acc_get(unsigned alo, unsigned ahi) {
-    unsigned lo, hi;
-    asm("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(alo));
-    asm("v_accvgpr_read_b32 %0, %1" : "=v"(hi) : "a"(ahi));
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
 // entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane =
 // original row), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
-#ifndef BR_LU_CH
-#define BR_LU_CH 8   // 4: 63.9k, 2: 62.8k, 8: 64.1k GRI reactors/s (scalar branch per chunk)
-#endif
+// Live columns go in chunks of 8 (measured round 1: 4: 63.9k, 2: 62.8k, 8: 64.1k GRI reactors/s).
 template <int W>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
-                                            double& dinv, int& fail, const LUWs& F, LDSd* pr) {
-    constexpr int CH = BR_LU_CH;   // live-column granularity of the rank-1 update
+                                            double& dinv, int& fail, const LUWs& F) {
+    constexpr int CH = 8;   // live-column granularity of the rank-1 update
     static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
@@ -1101,103 +1029,17 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
         F.M[k * WAVE + lane] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
         if (isp) { pstep = k; dinv = rinv; }
         const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
-#if BR_LU_LDSB
-        if (isp) prow_put<W>(pr, a, 1, live);
-        wave_sync();
-#endif
 #pragma unroll
         for (int c = 0; c < W; c += CH) {
             if (c < live) {
 #pragma unroll
                 for (int i = 0; i < CH; ++i) {
                     const int j = c + i;
-#if BR_LU_LDSB
-                    if (j + 1 < W) a[j] = fma(-(double)pr[j], l, a[j + 1]);
-#else
                     if (j + 1 < W) a[j] = fma(-bcast_lu(a[j + 1], p), l, a[j + 1]);
-#endif
                     else a[j] = 0.0;
                 }
             }
         }
-#if BR_LU_LDSB
-        wave_sync();
-#endif
-    }
-}
-
-// ---- pivot rows through LDS, one step ahead (BR_LU_LA) ----------------------------------
-// The rank-1 update needs the pivot row a_p[k+1..] in every lane. Broadcasting it element by
-// element costs two v_readlane + the FMA per element (3 VALU ops, the LU's main cost); through
-// LDS it costs one FMA per element plus LDS traffic, but a write-then-read round trip per step
-// on the elimination chain was measured slower (BR_LU_LDSB). Here the round trip is taken off
-// the chain: step k updates its first chunk of 8 columns, runs the pivot search for step k+1
-// on the updated column k+1, and from then on the NEW pivot lane stores each chunk of its row
-// into the other LDS buffer as soon as step k has updated it; step k+1 reads the row from
-// there (written chunks earlier). Two buffers alternate, so a step's reads never meet the
-// next step's writes (chunk order = program order, kept by scheduling barriers; LDS executes a
-// wave's accesses in order). The arithmetic (pivot choice,
-// multipliers, FMA order) is that of lu_rl_steps.
-#ifndef BR_LU_LA
-#define BR_LU_LA 0   // measured: GRI 79.4k vs 92.4k, surf 165k vs 192k reactors/s (a broadcast LDS read moves 512 B per wave: LDS-bandwidth-bound, 2x the readlane cost per CU)
-#endif
-template <int W>
-__device__ __forceinline__ void lu_la_step(double (&a)[W], int k, int k1, int cend, int lane, int& pstep,
-                                           double& dinv, int& fail, const LUWs& F, const LDSd* ub, LDSd* nb,
-                                           int& p, double& piv) {
-    constexpr int CH = 8;
-    if (piv == 0.0 && !fail) fail = k + 1;
-    const double rinv = 1.0 / piv;
-    const bool isp = (lane == p);
-    const bool rem = (pstep < 0) && !isp;
-    const double l = rem ? a[0] * rinv : 0.0;
-    F.M[k * WAVE + lane] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
-    if (isp) { pstep = k; dinv = rinv; }
-    const int live = cend - k;                 // columns k..cend-1 are live in a[0..live-1]
-    const bool more = k + 1 < k1;
-    int pn = 0;
-    double pivn = 1.0;
-#pragma unroll
-    for (int c = 0; c < W; c += CH) {
-        __builtin_amdgcn_sched_barrier(0);     // a chunk's row reads stay with its FMAs (registers)
-        if (c < live) {
-#pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const int j = c + i;
-                if (j + 1 < W) a[j] = fma(-(double)ub[j + 1], l, a[j + 1]);
-                else a[j] = 0.0;
-            }
-            if (more) {
-                if (c == 0) {                      // column k+1 is final for step k: next pivot
-                    pn = pivot_lane(fabs(a[0]), pstep < 0);
-                    pivn = bcast(a[0], pn);
-                }
-                if (lane == pn) {
-#pragma unroll
-                    for (int i = 0; i < CH; ++i) nb[c + i] = a[c + i];
-                }
-            }
-        }
-    }
-    p = pn;
-    piv = pivn;
-}
-// steps k0..k1-1; on entry the pivot of step k0 is not yet known (prologue: search + row store)
-template <int W>
-__device__ __forceinline__ void lu_la_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
-                                            double& dinv, int& fail, const LUWs& F, LDSd* bufA, LDSd* bufB) {
-    int p = pivot_lane(fabs(a[0]), pstep < 0);
-    double piv = bcast(a[0], p);
-    if (lane == p) {
-#pragma unroll
-        for (int j = 0; j < W; ++j) bufA[j] = a[j];
-    }
-    LDSd* ub = bufA;
-    LDSd* nb = bufB;
-#pragma unroll 1
-    for (int k = k0; k < k1; ++k) {
-        lu_la_step<W>(a, k, k1, cend, lane, pstep, dinv, fail, F, ub, nb, p, piv);
-        LDSd* t = ub; ub = nb; nb = t;
     }
 }
 
@@ -1221,12 +1063,13 @@ __device__ __forceinline__ double lane_pull(double v, int src) {
 // is factored right-looking. The arithmetic is exactly that of the unblocked right-looking LU.
 // Finally the rows of M are permuted into step order in place (gather, then store), and D^-1
 // is stored in step order. Returns 0 or k+1 for a zero pivot; *perm_out = pivot_perm.
-template <int NMAX, bool ACC = false>
+template <int NMAX>
 __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
-                                         int lane, int& perm_out, LDSd* pr, AccFac<NMAX>* af = nullptr) {
+                                         int lane, int& perm_out) {
     constexpr int P = NMAX < 32 ? NMAX : 32;
     constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
     constexpr int CH = 8;
+    static_assert(NMAX % CH == 0 && NMAX <= 64, "lu_factor: NMAX");
     const BR_GLOBAL double* J = launder(J_);
     BR_GLOBAL double* wsg = launder(ws);
     const LUWs F{wsg, wsg + NMAX * WAVE};
@@ -1244,11 +1087,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (j < n && act) ? J[j * WAVE + lane] : 0.0;
             a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
         }
-#if BR_LU_LA
-        lu_la_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F, pr, pr + 64);
-#else
-        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F, pr);
-#endif
+        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F);
     }
     BR_SUB_ADD(0, lt0);
     BR_SUB_T(lt1);
@@ -1260,69 +1099,29 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (col < n && act) ? J[col * WAVE + lane] : 0.0;
             b[j] = ((col == lane) ? 1.0 : 0.0) - gamma * jv;
         }
-        // (BR_LU_LA: multipliers prefetched 4 steps ahead instead of 8; the LDS row chunk takes the
-        // registers the readlane broadcast kept in SGPRs)
-        constexpr int LL = BR_LU_LA ? 4 : CH;
-        double cur[LL], nxt[LL];
+        // multipliers of panel 1 re-read from M, one chunk of CH steps ahead
+        double cur[CH], nxt[CH];
 #pragma unroll
-        for (int i = 0; i < LL; ++i) cur[i] = F.M[i * WAVE + lane];
-#if BR_LU_LA
-        // pivot rows of the left-looking steps through LDS, one step ahead (see lu_la_step): the
-        // pivot lane of step k+1 (pstep == k+1) stores each chunk of its row once step k updated it
-        LDSd* const lb0 = pr;
-        LDSd* const lb1 = pr + 64;
-        if (pstep == 0) {
-#pragma unroll
-            for (int j = 0; j < W2; ++j) lb0[j] = b[j];
-        }
-#endif
+        for (int i = 0; i < CH; ++i) cur[i] = F.M[i * WAVE + lane];
 #pragma unroll 1
-        for (int kb = 0; kb < P; kb += LL) {
-            if (kb + LL < P) {
+        for (int kb = 0; kb < P; kb += CH) {
+            if (kb + CH < P) {
 #pragma unroll
-                for (int i = 0; i < LL; ++i) nxt[i] = F.M[(kb + LL + i) * WAVE + lane];
+                for (int i = 0; i < CH; ++i) nxt[i] = F.M[(kb + CH + i) * WAVE + lane];
             }
 #pragma unroll
-            for (int i = 0; i < LL; ++i) {
+            for (int i = 0; i < CH; ++i) {
                 const int k = kb + i;
-#if BR_LU_LA
-                const LDSd* ub = (i & 1) ? lb1 : lb0;    // static parity (kb is a multiple of LL, even)
-                LDSd* nb = (i & 1) ? lb0 : lb1;
-                const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
-                const bool nxp = (pstep == k + 1);
-#pragma unroll
-                for (int c = 0; c < W2; c += 8) {
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = c; j < c + 8 && j < W2; ++j) b[j] = fma(-(double)ub[j], l, b[j]);
-                    if (nxp) {
-#pragma unroll
-                        for (int j = c; j < c + 8 && j < W2; ++j) nb[j] = b[j];
-                    }
-                }
-#elif BR_LU_LDSB
-                if (pstep == k) prow_put<W2>(pr, b, 0, W2);
-                wave_sync();
-                const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
-#pragma unroll
-                for (int j = 0; j < W2; ++j) b[j] = fma(-(double)pr[j], l, b[j]);
-                wave_sync();
-#else
                 const unsigned long long m = __ballot(pstep == k);
                 const int p = (int)__builtin_ctzll(m);
                 const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
 #pragma unroll
                 for (int j = 0; j < W2; ++j) b[j] = fma(-bcast_lu(b[j], p), l, b[j]);
-#endif
             }
 #pragma unroll
-            for (int i = 0; i < LL; ++i) cur[i] = nxt[i];
+            for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
         }
-#if BR_LU_LA
-        lu_la_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F, pr, pr + 64);
-#else
-        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F, pr);
-#endif
+        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F);
     }
     BR_SUB_ADD(1, lt1);
     BR_SUB_T(lt2);
@@ -1342,143 +1141,25 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             if (t + 1 < NC) gather(g[(t + 1) & 1], (t + 1) * CH);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const double v = (t * CH + i < n) ? g[t & 1][i] : 0.0;
-                if constexpr (ACC) acc_put(af->lo[t * CH + i], af->hi[t * CH + i], v);
-                else F.M[(t * CH + i) * WAVE + lane] = v;
-            }
+            for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * WAVE + lane] = (t * CH + i < n) ? g[t & 1][i] : 0.0;
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    if constexpr (ACC) acc_put(af->dlo, af->dhi, lane_pull(dinv, perm));
-    else F.D[lane] = lane_pull(dinv, perm);
+    F.D[lane] = lane_pull(dinv, perm);
     BR_SUB_ADD(2, lt2);
     perm_out = perm;
     return fail;
 }
 
-// solve with the AGPR-resident factors (same arithmetic and order as lu_solve): the forward
-// sweep over columns k (rows s > k), D^-1, the backward sweep (rows s < k); per column the only
-// dependency chain is readlane(r, k) -> fma, the factor reads and lane masks are off it
-template <int NMAX>
-__device__ __forceinline__ double lu_solve_acc(const AccFac<NMAX>& af, int n, int lane, int perm, double b) {
-    double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
-    const int lo = (lane < n) ? lane : -1;
-#pragma unroll
-    for (int k = 0; k < NMAX; ++k) {
-        const double v = acc_get(af.lo[k], af.hi[k]);
-        const double vm = (lo > k) ? v : 0.0;
-        r = fma(-vm, bcast(r, k < n ? k : 0), r);
-    }
-    r *= acc_get(af.dlo, af.dhi);
-#pragma unroll
-    for (int k = NMAX - 1; k >= 0; --k) {
-        const double v = acc_get(af.lo[k], af.hi[k]);
-        const double vm = (lane < ((k < n) ? k : 0)) ? v : 0.0;
-        r = fma(-vm, bcast(r, k < n ? k : 0), r);
-    }
-    return (lane < n) ? r : 0.0;
-}
-
-// one triangular sweep over step-ordered factor columns in chunks of 8 (forward: k ascending,
-// rows s > k; backward: k descending, rows s < k): r[s] -= M[s][k] * r[k], for k < n only.
-// Loads are unconditional (so the compiler's vmcnt waits stay exact and the prefetch is real):
-// rows a chunk cannot touch re-read a row it does touch (same 128-B lines, no extra traffic)
-// and columns past n re-read column n-1; the per-column lane masks discard what they feed.
-// Two register buffers alternate: each chunk's loads are issued a full chunk ahead of use.
-#ifndef BR_TRI_DIAG
-#define BR_TRI_DIAG 1   // masked-out lanes load the (zero) diagonal entry instead of being masked
-#endif
-// Diagonal-redirect form (BR_TRI_DIAG): the step-ordered factor matrix holds an exact 0 at (k, k)
-// and in every row >= n, so a lane that must not update in column k loads row k of that column:
-// row = max(lane, k) in the forward sweep (rows > k update), min(lane, k) in the backward sweep
-// (rows < k). The loaded factor is then the masked one, with no compare/select per column, and
-// row k shares a 128-B line with the rows that do update except at 3 line boundaries.
-template <bool FWD>
-__device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned lane8) {
-    // raw buffer loads: per-lane offset max/min(lane, k) * 8 in the VGPR, the chunk's column base
-    // c * 512 B in soffset and the column within the chunk as the immediate (<= 3584 B): one VALU
-    // op per column and no per-column 64-bit address arithmetic
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const unsigned k8 = (unsigned)(c + i) * 8u;
-        const unsigned off = FWD ? max(lane8, k8) : min(lane8, k8);
-        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (WAVE * 8), c * (WAVE * 8), 0));
-    }
-}
-template <bool FWD>
-__device__ __forceinline__ void tri_chunk_diag(const double (&v)[8], int c, int n, double& r) {
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii) {
-        const int i = FWD ? ii : 7 - ii;
-        const int k = c + i;
-        r = fma(-v[i], bcast(r, k), r);   // k >= n: a padding column of zeros, x finite
-    }
-}
-template <bool FWD>
-__device__ __forceinline__ void tri_chunk(const double (&v)[8], int c, int lo, int n, double& r) {
-    // the lane masks zero the factor entries up front (off the r dependency chain): a lane that
-    // must not update adds -0 * x, which leaves r unchanged, so the chain per column is just
-    // fma -> readlane -> fma (x = r[k] is finite whenever the solve is)
-    double vm[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int k = c + i;
-        // forward: lo = lane (lanes >= n: -1); backward: lo = lane, limit min(k, n) with k >= n -> none
-        const bool upd = FWD ? (lo > k) : (lo < ((k < n) ? k : 0));
-        vm[i] = upd ? v[i] : 0.0;
-    }
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii) {
-        const int i = FWD ? ii : 7 - ii;
-        const int k = c + i;
-        const double x = bcast(r, k < n ? k : 0);
-        r = fma(-vm[i], x, r);
-    }
-}
-template <bool FWD>
-__device__ __forceinline__ void tri_load(double (&v)[8], const BR_GLOBAL double* __restrict__ col, int c, int lane,
-                                         int n) {
-    // columns [n, roundup8(n)) are stored as zeros; later chunks are in bounds and masked
-    const int row = FWD ? min(max(lane, c + 1), n - 1) : min(min(lane, c + 7), n - 1);
-    const BR_GLOBAL double* p = col + c * WAVE + row;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = p[i * WAVE];
-}
-#ifndef BR_TRI_DEPTH
-#define BR_TRI_DEPTH 3   // register buffers of 8 columns in flight (loads DEPTH-1 chunks ahead)
-#endif
-template <bool FWD, int NCH>
-__device__ __forceinline__ double tri_sweep(const BR_GLOBAL double* __restrict__ col, int lane, int n, double r) {
-    constexpr int DB = BR_TRI_DEPTH;
-    double A[DB][8];
-    auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
-    const int lo = FWD ? ((lane < n) ? lane : -1) : lane;
-#pragma unroll
-    for (int t = 0; t < DB - 1; ++t)
-        if (t < NCH) tri_load<FWD>(A[t], col, cidx(t), lane, n);
-#pragma unroll
-    for (int t = 0; t < NCH; ++t) {          // fully unrolled: exact vmcnt waits for the prefetch
-        __builtin_amdgcn_sched_barrier(0);   // loads stay DB-1 chunks ahead of their use
-        if (t + DB - 1 < NCH) tri_load<FWD>(A[(t + DB - 1) % DB], col, cidx(t + DB - 1), lane, n);
-        __builtin_amdgcn_sched_barrier(0);
-        tri_chunk<FWD>(A[t % DB], cidx(t), lo, n, r);
-    }
-    return r;
-}
-
-// ---- DPP form of the triangular sweeps (BR_TRI_DPP): the columns go in blocks of 16, one block
-// per 16-lane DPP row. Block b first runs its diagonal 16 x 16 part inside row b: r += -M[s][k] *
-// r[k], with r[k] broadcast from lane k of the row by the DPP modifier of the FMA itself
-// (v_fmac_f64 row_newbcast) and the write limited to row b by the DPP row mask: one VALU op per
-// column instead of two v_readlane + FMA, no exec change, no branch. The finished values of row
-// b are then copied to every row through LDS (one write, one read) and the rows below (forward)
-// / above (backward) apply the block's columns with the same DPP FMA on the copy. Every lane
-// still accumulates its columns in the same order with the same fma(-M[s][k], r[k], r[s]), so
-// the result is bit-identical to tri_chunk_diag's.
-#ifndef BR_TRI_DPP
-#define BR_TRI_DPP 1
-#endif
+// ---- triangular sweeps in DPP form: the columns go in blocks of 16, one block per 16-lane DPP
+// row. Block b first runs its diagonal 16 x 16 part inside row b: r += -M[s][k] * r[k], with r[k]
+// broadcast from lane k of the row by the DPP modifier of the FMA itself (v_fmac_f64
+// row_newbcast) and the write limited to row b by the DPP row mask: one VALU op per column
+// instead of two v_readlane + FMA, no exec change, no branch. The finished values of row b are
+// then copied to every row through LDS (one write, one read) and the rows below (forward) /
+// above (backward) apply the block's columns with the same DPP FMA on the copy. Every lane
+// accumulates its columns in column order with fma(-M[s][k], r[k], r[s]), i.e. the arithmetic
+// of a plain column-oriented substitution (bit-identical to the readlane form).
 // r += -f * r[row base + K] in the rows of RM; the s_nop covers the VALU-write -> DPP-read
 // hazard on r (the previous op of the chain wrote it)
 template <int K, int RM>
@@ -1508,9 +1189,24 @@ __device__ __forceinline__ void dpp_off(double& r, double x, const double (&v)[1
         dpp_off<FWD, CW, RM, I + 1>(r, x, v);
     }
 }
+// Diagonal-redirect loads: the step-ordered factor matrix holds an exact 0 at (k, k) and in every
+// row >= n, so a lane that must not update in column k loads row k of that column: row =
+// max(lane, k) in the forward sweep (rows > k update), min(lane, k) in the backward sweep (rows
+// < k). The loaded factor is then the masked one, with no compare/select per column, and row k
+// shares a 128-B line with the rows that do update except at 3 line boundaries. Raw buffer
+// loads: per-lane offset in the VGPR (one v_max / v_min per column), the chunk's column base
+// c * 512 B in soffset and the column within the chunk as the immediate (<= 3584 B).
+template <bool FWD>
+__device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned lane8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const unsigned k8 = (unsigned)(c + i) * 8u;
+        const unsigned off = FWD ? max(lane8, k8) : min(lane8, k8);
+        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (WAVE * 8), c * (WAVE * 8), 0));
+    }
+}
 // block T of a sweep (blocks of 16 columns, the last one NMAX % 16 wide if that is not 0),
-// factor loads one block ahead (diagonal-redirect offsets, see tri_load_diag); x64 = 64 doubles
-// of LDS scratch
+// factor loads one block ahead; x64 = 64 doubles of LDS scratch
 template <bool FWD, int NMAX, int T>
 __device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigned lane8, double& r, LDSd* x64,
                                               double (&v)[2][16]) {
@@ -1549,65 +1245,25 @@ __device__ __forceinline__ void tri_sweep_dpp(__amdgpu_buffer_rsrc_t rs, int lan
 
 // solve (I - gamma J) x = b with the factors of lu_factor: L y = P b, y' = D^-1 y, U' x = y'.
 // `perm` from lu_factor; b and the returned x are in natural component order (the backward
-// sweep leaves unknown s, i.e. column s, on lane s).
+// sweep leaves unknown s, i.e. column s, on lane s). x16: 64 doubles of LDS scratch.
 template <int NMAX>
 __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n, int lane, int perm, double b,
                                            LDSd* x16) {
+    static_assert(NMAX % 8 == 0 && NMAX <= 64, "lu_solve: NMAX");
     const BR_GLOBAL double* wsg = launder(ws);
     lane = launder_v(lane);
-#if BR_TRI_DPP
-    if constexpr (NMAX % 8 == 0) {
-        // one buffer descriptor over factors + D^-1: every load of the solve is a buffer load, so
-        // the waitcnt pass can count them in order (a global load among them forces vmcnt(0))
-        // (and nothing issued before the solve may still be pending: a flat or scratch access of the
-        // controller would make the counter out of order too -- so drain it first)
-        __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0)
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * WAVE * 8, 0x00020000);
-        const double dinv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * WAVE * 8, 0));
-        double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
-        tri_sweep_dpp<true, NMAX>(rs, lane, r, x16);
-        r *= dinv;
-        tri_sweep_dpp<false, NMAX>(rs, lane, r, x16);   // (x16: 64 doubles of LDS scratch)
-        return (lane < n) ? r : 0.0;
-    }
-#endif
-    // the forward (unit lower) and backward (unit upper) sweeps run as ONE chunk sequence with
-    // one prefetch pipeline, so the backward sweep's first columns and D^-1 are already in
-    // flight while the forward sweep finishes (the factors come from L2 / Infinity Cache)
-    constexpr int NCH = NMAX / 8, NT = 2 * NCH, DB = BR_TRI_DEPTH;
-    double A[DB][8];
-    const unsigned lane8 = (unsigned)lane * 8u;
-    // buffer descriptor over the factor matrix (gfx9 dword 3; records = its byte size)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, NMAX * WAVE * 8, 0x00020000);
-    auto load = [&](int t) {
-#if BR_TRI_DIAG
-        if (t < NCH) tri_load_diag<true>(A[t % DB], rs, t * 8, lane8);
-        else tri_load_diag<false>(A[t % DB], rs, (NT - 1 - t) * 8, lane8);
-#else
-        if (t < NCH) tri_load<true>(A[t % DB], wsg, t * 8, lane, n);
-        else tri_load<false>(A[t % DB], wsg, (NT - 1 - t) * 8, lane, n);
-#endif
-    };
-    const double dinv = wsg[NMAX * WAVE + lane];   // D^-1
+    // one buffer descriptor over factors + D^-1: every load of the solve is a buffer load, so the
+    // waitcnt pass can count them in order (a global load among them forces vmcnt(0)); nothing
+    // issued before the solve may still be pending either (a flat or scratch access of the
+    // controller would make the counter out of order too), so drain it first
+    __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * WAVE * 8, 0x00020000);
+    const double dinv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * WAVE * 8, 0));
     double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
-    const int lo = (lane < n) ? lane : -1;
-#pragma unroll
-    for (int t = 0; t < DB - 1; ++t) load(t);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + DB - 1 < NT) load(t + DB - 1);
-        __builtin_amdgcn_sched_barrier(0);
-#if BR_TRI_DIAG
-        if (t < NCH) tri_chunk_diag<true>(A[t % DB], t * 8, n, r);
-        else tri_chunk_diag<false>(A[t % DB], (NT - 1 - t) * 8, n, r);
-#else
-        if (t < NCH) tri_chunk<true>(A[t % DB], t * 8, lo, n, r);
-        else tri_chunk<false>(A[t % DB], (NT - 1 - t) * 8, lane, n, r);
-#endif
-        if (t == NCH - 1) r *= dinv;
-    }
+    tri_sweep_dpp<true, NMAX>(rs, lane, r, x16);
+    r *= dinv;
+    tri_sweep_dpp<false, NMAX>(rs, lane, r, x16);
     return (lane < n) ? r : 0.0;
 }
 
@@ -1793,100 +1449,15 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
     return fail;
 }
 
-// forward / backward sweeps over the step-ordered 128-row columns (fully unrolled: the column
-// of every FMA, and so the lane and row set holding r[k], are compile-time constants)
-template <bool FWD, int NMAX>
-__device__ __forceinline__ void tri_sweep2_diag(const BR_GLOBAL double* __restrict__ col, int lane, int n,
-                                                double (&r)[2]) {
-    // diagonal-redirect loads (see tri_load_diag): the step-ordered factor matrix is 0 at (k, k)
-    // and in every row >= n; first-half rows use max/min(row, k); second-half rows that cannot
-    // update are sent to k (backward) or, in the forward sweep, clamped into the 128-B line of
-    // rows 64..79, whose rows >= n (n <= 72) are zero -- so no extra lines and no selects
-    constexpr int JW = 128, NCH = NMAX / 8;
-    static_assert(NMAX <= 72, "rows n..79 must be padding");
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)col, (short)0, NMAX * JW * 8, 0x00020000);
-    const unsigned lane8 = (unsigned)lane * 8u, hi8 = lane8 + 512u;
-    double v[2][2][8];
-    auto load = [&](double (&b)[2][8], int c) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const unsigned k8 = (unsigned)(c + i) * 8u;
-            const unsigned o0 = FWD ? max(lane8, k8) : min(lane8, k8);
-            const unsigned o1 = FWD ? min(max(hi8, k8), 79u * 8u) : min(hi8, k8);
-            const int cb = (c + i) * JW * 8;
-            b[0][i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, 0));
-            b[1][i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, cb, 0));
-        }
-    };
-    auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
-    load(v[0], cidx(0));
-    if (NCH > 1) load(v[1], cidx(1));
-#pragma unroll
-    for (int t = 0; t < NCH; ++t) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int c = cidx(t);
-#pragma unroll
-        for (int ii = 0; ii < 8; ++ii) {
-            const int i = FWD ? ii : 7 - ii;
-            const int k = c + i;
-            const double x = bcast(r[k >> 6], k & 63);   // padding columns: x finite, factors 0
-#pragma unroll
-            for (int s = 0; s < 2; ++s) r[s] = fma(-v[t & 1][s][i], x, r[s]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 2 < NCH) load(v[t & 1], cidx(t + 2));
-    }
-}
-template <bool FWD, int NMAX>
-__device__ __forceinline__ void tri_sweep2(const BR_GLOBAL double* __restrict__ col, int lane, int n, double (&r)[2]) {
-    constexpr int JW = 128, NCH = NMAX / 8;
-    double v[2][2][8];
-    const int row0 = min(lane, n - 1), row1 = min(lane + 64, n - 1);
-    auto load = [&](double (&b)[2][8], int c) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            b[0][i] = col[(c + i) * JW + row0];
-            b[1][i] = col[(c + i) * JW + row1];
-        }
-    };
-    auto cidx = [&](int t) { return FWD ? t * 8 : (NCH - 1 - t) * 8; };
-    load(v[0], cidx(0));
-    if (NCH > 1) load(v[1], cidx(1));
-#pragma unroll
-    for (int t = 0; t < NCH; ++t) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int c = cidx(t);
-        // masks applied to the factor entries, off the r chain (see tri_chunk)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int k = c + i;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int row = lane + 64 * s;
-                const bool upd = FWD ? (row > k && row < n) : (row < k && k < n);
-                v[t & 1][s][i] = upd ? v[t & 1][s][i] : 0.0;
-            }
-        }
-#pragma unroll
-        for (int ii = 0; ii < 8; ++ii) {
-            const int i = FWD ? ii : 7 - ii;
-            const int k = c + i;
-            const double x = bcast(r[k >> 6], k & 63);
-#pragma unroll
-            for (int s = 0; s < 2; ++s) r[s] = fma(-v[t & 1][s][i], x, r[s]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 2 < NCH) load(v[t & 1], cidx(t + 2));
-    }
-}
-
-// DPP form of the CPL = 2 sweeps (BR_TRI_DPP; 64 < n <= NMAX = 72): r0 holds row lane, r1 row lane + 64
+// Triangular sweeps of the CPL = 2 factors in DPP form (64 < n <= NMAX = 72): r0 holds row lane, r1 row lane + 64
 // (lanes 0..NMAX-65 real, the rest of DPP row 0 is zero padding). Column blocks 0..3 are rows 0..63 in r0
 // (DPP row b), block 4 = columns 64..NMAX-1 is DPP row 0 of r1. Forward: block b's diagonal part in
 // row b of r0, its finished values copied to every row through LDS, then the rows of r0 below it and
 // the r1 rows (all below) apply it; block 4 last, inside r1. Backward: block 4 first inside r1, its
-// values applied to every r0 row, then blocks 3..0 in r0 (r1 rows are below them: untouched). Same
-// per-lane FMA order as tri_sweep2_diag, so bit-identical.
+// values applied to every r0 row, then blocks 3..0 in r0 (r1 rows are below them: untouched).
+// Factor loads: diagonal redirect (the step-ordered matrix is 0 at (k, k) and in every row >= n;
+// first-half rows use max/min(row, k); second-half rows that cannot update are sent to k
+// (backward) or, forward, clamped into the 128-B line of rows 64..79, whose rows >= n are zero).
 template <bool FWD, int CW>
 __device__ __forceinline__ void tri2_load_blk(double (&v0)[16], double (&v1)[16], __amdgpu_buffer_rsrc_t rs, int c0,
                                               unsigned lane8, unsigned hi8, bool want0, bool want1) {
@@ -1990,33 +1561,15 @@ __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* s
     wave_sync();
     double r[2] = {dsc[perm[0]], dsc[perm[1]]};   // P b
     wave_sync();
-#if BR_TRI_DPP
-    if constexpr (NMAX > 64 && NMAX <= 72) {
-        // (all solve loads are buffer loads: drain first so the waitcnt pass can count them in order)
-        __builtin_amdgcn_s_waitcnt(0x70);
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * JW * 8, 0x00020000);
-        const double dv[2] = {
-            __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * JW * 8, 0)),
-            __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8 + 512, NMAX * JW * 8, 0))};
-        tri_sweeps2_dpp<NMAX>(rs, lane, r, dv, scr);
-        b[0] = (lane < n) ? r[0] : 0.0;
-        b[1] = (lane + 64 < n) ? r[1] : 0.0;
-        return;
-    }
-#endif
-#if BR_TRI_DIAG
-    tri_sweep2_diag<true, NMAX>(wsg, lane, n, r);
-#else
-    tri_sweep2<true, NMAX>(wsg, lane, n, r);
-#endif
-    r[0] *= wsg[NMAX * JW + lane];
-    r[1] *= wsg[NMAX * JW + 64 + lane];
-#if BR_TRI_DIAG
-    tri_sweep2_diag<false, NMAX>(wsg, lane, n, r);
-#else
-    tri_sweep2<false, NMAX>(wsg, lane, n, r);
-#endif
+    static_assert(NMAX > 64 && NMAX <= 72, "lu_solve2: NMAX");
+    // (all solve loads are buffer loads: drain first so the waitcnt pass can count them in order)
+    __builtin_amdgcn_s_waitcnt(0x70);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * JW * 8, 0x00020000);
+    const double dv[2] = {
+        __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * JW * 8, 0)),
+        __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8 + 512, NMAX * JW * 8, 0))};
+    tri_sweeps2_dpp<NMAX>(rs, lane, r, dv, scr);
     b[0] = (lane < n) ? r[0] : 0.0;
     b[1] = (lane + 64 < n) ? r[1] : 0.0;
 }

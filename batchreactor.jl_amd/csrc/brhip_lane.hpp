@@ -700,6 +700,13 @@ __device__ __forceinline__ int l_post_solve(LCV& c, ZH<NM>& z, double (&acor)[NM
     for (int i = 0; i < NM; ++i) acor[i] *= c.tq[2];
     c.nstloc += 1;
     c.eta = eta; c.hprime = hprime; c.qprime = qprime;
+    {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor);
+        // first, as in the oracle: an unstable step writes no dense output
+        double zm = 0.0;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) { const double a = fabs(z.z0[i]); zm = fmax(zm, a == a ? a : INFINITY); }
+        if (!(zm < INFINITY) || zm > c.ulimit) { c.status = BR_ERR_UNSTABLE; return A_DONE; }
+    }
     if (o.ign >= 0) {                            // ignition marker (midpoint of the steepest step)
         const double x = l_mole_frac<NM>(z.z0, n, o.ign);
         const double r = (x - c.ign_x) / (c.tn - c.ign_t);
@@ -723,12 +730,6 @@ __device__ __forceinline__ int l_post_solve(LCV& c, ZH<NM>& z, double (&acor)[NM
 #pragma unroll
         for (int i = 0; i < NM; ++i) if (i < n) row[i] = yo[i];
         c.iout += 1;
-    }
-    {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor)
-        double zm = 0.0;
-#pragma unroll
-        for (int i = 0; i < NM; ++i) { const double a = fabs(z.z0[i]); zm = fmax(zm, a == a ? a : INFINITY); }
-        if (!(zm < INFINITY) || zm > c.ulimit) { c.status = BR_ERR_UNSTABLE; return A_DONE; }
     }
     const double tn = c.tn;
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));

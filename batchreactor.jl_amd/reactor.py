@@ -210,10 +210,15 @@ def batch_reactor(input_file, lib_dir, udf=None, *, sens=False, surfchem=False, 
     if sens:
         return _gpu_rhs_problem(mech, eng, T, Asv, u0, tf, chem)
     # one row per accepted step (save_data callback, :383-402): rho from the accepted state u,
-    # x, p and coverages from the step's last RHS evaluation (the engine's trace rows carry both);
-    # the trace holds max_steps rows, so one integration always covers the whole run
-    u, st, tr = eng.integrate([T], [Asv], u0[None, :], [tf], trace_cap=max_steps, max_steps=max_steps)
+    # x, p and coverages from the step's last RHS evaluation (the engine's trace rows carry both).
+    # The trace starts at 4096 rows; a run that took more steps is repeated once with exactly its
+    # step count (the integration is deterministic, so the repeat takes the same steps)
+    cap = min(4096, max_steps)
+    u, st, tr = eng.integrate([T], [Asv], u0[None, :], [tf], trace_cap=cap, max_steps=max_steps)
     nst = int(st["nsteps"][0])
+    if nst > cap:
+        u, st, tr = eng.integrate([T], [Asv], u0[None, :], [tf], trace_cap=nst, max_steps=max_steps)
+        nst = int(st["nsteps"][0])
     n, ng = mech.n, mech.ng
     streams = _open_streams(folder, mech, chem.surfchem)
     try:

@@ -10,7 +10,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-lib = C.CDLL(os.path.join(ROOT, "batchreactor.jl_amd", "libexp_lu.so"))
+lib = C.CDLL(os.path.join(ROOT, "scripts", "micro", "libexp_lu.so"))   # make -C scripts/micro libexp_lu.so
 lib.exp_lu_update.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int,
                               C.POINTER(C.c_float)]
 nmat = int(sys.argv[1]) if len(sys.argv) > 1 else 16384

@@ -667,6 +667,25 @@ def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
             assert 0.8 * so["nsteps"] <= st["nsteps"][i] <= 1.2 * so["nsteps"] + 40, (i, st["nsteps"][i], so["nsteps"])
 
 
+def test_lane_deferral_step_budget(pkg, orc, gpu, monkeypatch):
+    """The step limit holds for the whole run across the lane -> wavefront hand-over (SciML's
+    maxiters counts every step of one solve): with max_steps = 60 and deferral after 30 lane steps,
+    every reactor that needs more than 60 steps stops with BR_ERR_MAXSTEPS (-1) after exactly 60
+    steps in total -- the oracle's CVODE run reports the same status at the same step count."""
+    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    monkeypatch.setenv("BRHIP_DEFER_STEPS", "30")
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    assert eng.engine == "lane"
+    N = 64
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", N, 12)
+    U, st = eng.integrate(T, Asv, U0, 10.0, max_steps=60)
+    for i in range(N):
+        _, so, _ = om.integrate(T[i], Asv[i], U0[i], 10.0, analytic_jac=True, max_steps=60)
+        assert so["status"] == -1 and so["nsteps"] == 60
+        assert st["status"][i] == -1 and st["nsteps"][i] == 60, (i, st["status"][i], st["nsteps"][i])
+
+
 @pytest.mark.parametrize("case,N", [("gri", 3000), ("surf", 5000)])
 def test_persistent_grid_matches_static(pkg, gpu, monkeypatch, case, N):
     """k_integrate's persistent grid (waves take reactors from a work counter, reusing their LDS
