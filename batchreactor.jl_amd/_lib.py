@@ -33,11 +33,22 @@ class Opts(C.Structure):
 
 
 NSTAT = 20
+BATCH_MAXCOMP = 64
+
+
+class BatchInput(C.Structure):
+    """br_batch_input (br_read_batch_xml)"""
+    _fields_ = [("gas_mech", C.c_char * 256), ("surface_mech", C.c_char * 256), ("gasphase", C.c_char * 1024),
+                ("T", C.c_double), ("p", C.c_double), ("Asv", C.c_double), ("time", C.c_double),
+                ("has_T", C.c_int), ("has_p", C.c_int), ("has_Asv", C.c_int), ("has_time", C.c_int),
+                ("ncomp", C.c_int), ("comp_is_mass", C.c_int),
+                ("comp_names", (C.c_char * 32) * BATCH_MAXCOMP), ("comp_values", C.c_double * BATCH_MAXCOMP)]
 
 
 EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info", "br_mech_engine", "br_mech_launch_info",
            "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev",
-           "br_last_kernel_ms", "br_debug_lu_solve"]
+           "br_last_kernel_ms", "br_debug_lu_solve", "br_mech_parse", "br_host_mech_desc", "br_host_mech_sizes",
+           "br_host_mech_species", "br_host_mech_theta0", "br_host_mech_free", "br_mech_compile", "br_read_batch_xml"]
 
 _lib = None
 
@@ -69,8 +80,19 @@ def lib():
     L.br_last_kernel_ms.argtypes = [vp, dp]
     L.br_debug_lu_solve.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, ip]
     L.br_debug_lu_solve.restype = C.c_int
+    cs = C.c_char_p
+    L.br_mech_parse.argtypes = [cs, cs, cs, cs, C.c_int, C.POINTER(vp)]
+    L.br_host_mech_desc.argtypes = [vp, C.POINTER(MechDesc)]
+    L.br_host_mech_sizes.argtypes = [vp, ip, ip, ip, ip]
+    L.br_host_mech_species.argtypes = [vp, C.c_int, C.c_char_p, C.c_size_t]
+    L.br_host_mech_theta0.argtypes = [vp, dp]
+    L.br_host_mech_free.argtypes = [vp]
+    L.br_mech_compile.argtypes = [cs, cs, cs, cs, C.c_int, C.c_int, C.POINTER(vp)]
+    L.br_read_batch_xml.argtypes = [cs, C.POINTER(BatchInput)]
     for f in ("br_mech_create", "br_mech_destroy", "br_mech_info", "br_rates", "br_rhs", "br_jacobian",
-              "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev", "br_last_kernel_ms"):
+              "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev", "br_last_kernel_ms",
+              "br_mech_parse", "br_host_mech_desc", "br_host_mech_sizes", "br_host_mech_species",
+              "br_host_mech_theta0", "br_host_mech_free", "br_mech_compile", "br_read_batch_xml"):
         getattr(L, f).restype = C.c_int
     _lib = L
     return L

@@ -1267,6 +1267,8 @@ struct br_mech {
 };
 
 static thread_local std::string g_err;
+// error message from the host mechanism compiler (mech_host.cpp, same library)
+extern "C" __attribute__((visibility("hidden"))) void br_set_last_error(const char* msg) { g_err = msg; }
 static int fail(int code, const std::string& msg) { g_err = msg; return code; }
 static int fail_code_input() { return fail(BR_ERR_INPUT, "bad argument"); }
 #define HIPCHK(x)                                                                         \

@@ -7,6 +7,8 @@
  *   br_mech_create   <- compile_gaschemistry / SurfaceReactions.compile_mech /
  *                       IdealGas.create_thermo results (src/BatchReactor.jl:254,265,287):
  *                       the host flattens the compiled mechanism into br_mech_desc.
+ *   br_mech_parse /  <- the same three compilers reading the mechanism library files
+ *   br_mech_compile     (src/BatchReactor.jl:242-287); br_read_batch_xml <- input_data (:238-306)
  *   br_rates         <- GasphaseReactions.calculate_molar_production_rates!(g_state,gmd,thermo)
  *                       (call site src/BatchReactor.jl:355) and
  *                       SurfaceReactions.calculate_molar_production_rates!(s_state,thermo,smd)
@@ -128,6 +130,46 @@ const char* br_last_error(void);
 int         br_device_count(void);
 
 int br_mech_create(const br_mech_desc* desc, int device, br_mech** out);
+
+/* ---- host mechanism compiler (C++, no GPU): the data formats the reference reads, flattened into
+ * br_mech_desc. Replaces, as one step:
+ *   compile_gaschemistry(get_path(lib_dir, <gas_mech>))       src/BatchReactor.jl:251-255
+ *   IdealGas.create_thermo(gasphase, get_path(lib_dir, "therm.dat"))                   :242-243,:265
+ *   SurfaceReactions.compile_mech(get_path(lib_dir, <surface_mech>), thermo, gasphase) :283-287
+ * gas_mech_path: CHEMKIN-II mechanism, or NULL/"" for surface-only runs, whose gas species are then
+ * the space-separated names of `gasphase` (the <gasphase> tag, :256-260). surf_mech_path: surface
+ * XML or NULL. conv: BR_CONV_* bits (BR_CONV_REFERENCE = the reference's gas kinetics). The
+ * tables are bit-identical to the Python host compiler's (batchreactor.jl_amd/mechanism.py). */
+typedef struct br_host_mech br_host_mech;
+int br_mech_parse(const char* gas_mech_path, const char* therm_path, const char* surf_mech_path,
+                  const char* gasphase, int conv, br_host_mech** out);
+/* desc's pointers point into h: valid until br_host_mech_free(h) */
+int br_host_mech_desc(const br_host_mech* h, br_mech_desc* desc);
+int br_host_mech_sizes(const br_host_mech* h, int* ng, int* ns, int* nrg, int* nrs);
+/* name of species i (gas species 0..ng-1 in mechanism order, then surface species), upper case */
+int br_host_mech_species(const br_host_mech* h, int i, char* buf, size_t n);
+/* initial coverages of the surface species (<site><initial>, the u0 tail of :228-230) */
+int br_host_mech_theta0(const br_host_mech* h, double* theta0 /*[ns]*/);
+int br_host_mech_free(br_host_mech* h);
+/* br_mech_parse + br_mech_create in one call */
+int br_mech_compile(const char* gas_mech_path, const char* therm_path, const char* surf_mech_path,
+                    const char* gasphase, int conv, int device, br_mech** out);
+
+/* batch.xml (input_data, src/BatchReactor.jl:238-306; schema docs/src/index.md:80-123). Asv is 1
+ * when the tag is missing (the reference's behaviour). The composition is the
+ * <molefractions> list (comp_is_mass = 0) or else <massfractions> (1), names upper case. */
+#define BR_BATCH_MAXCOMP 64
+typedef struct br_batch_input {
+    char gas_mech[256];
+    char surface_mech[256];
+    char gasphase[1024];      /* space-separated gas species names (surface-only runs) */
+    double T, p, Asv, time;
+    int has_T, has_p, has_Asv, has_time;
+    int ncomp, comp_is_mass;
+    char comp_names[BR_BATCH_MAXCOMP][32];
+    double comp_values[BR_BATCH_MAXCOMP];
+} br_batch_input;
+int br_read_batch_xml(const char* path, br_batch_input* out);
 int br_mech_destroy(br_mech* m);
 int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs);
 /* integrator engine br_integrate* uses for this mechanism: 0 = one reactor per wavefront

@@ -6,6 +6,8 @@
 # reltol=1e-6, abstol=1e-10)` of src/BatchReactor.jl:138-141,:204-210.
 module BatchReactorHIP
 
+using Printf
+
 const lib = joinpath(@__DIR__, "..", "batchreactor.jl_amd", "libbrhip.so")
 
 # convention bits (br_mech_desc.conv); REFERENCE = what GasphaseReactions does (DESIGN.md section 1)
@@ -64,7 +66,8 @@ const STAT_FIELDS = (:nsteps, :nfe, :nje, :nsetups, :nni, :ncfn, :netf, :status,
 last_error() = unsafe_string(ccall((:br_last_error, lib), Cstring, ()))
 check(rc) = rc == 0 || error("libbrhip error $rc: " * last_error())
 
-"""Create the device-resident mechanism (br_mech_create). `desc` must stay alive for the call."""
+"""Create the device-resident mechanism (br_mech_create). `desc` (and the arrays it points to) must
+stay alive for the call; the handle copies the tables to the GPU."""
 function mech_create(desc::Ref{BrMechDesc}, device::Integer=0)
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:br_mech_create, lib), Cint, (Ref{BrMechDesc}, Cint, Ref{Ptr{Cvoid}}), desc, device, h))
@@ -98,6 +101,222 @@ function integrate_traced!(m::Ptr{Cvoid}, T, Asv, u::Matrix{Float64}, tf; cap::I
     return stats, trace
 end
 
+# ---------------------------------------------------------------------------------------------
+# host mechanism compiler and batch.xml reader of libbrhip.so (C++; br_mech_parse, br_read_batch_xml):
+# the Julia host needs no Python and no chemistry package to build the tables
+# ---------------------------------------------------------------------------------------------
+const R_GAS = 8.31446261815324        # RxnHelperUtils.R (src/BatchReactor.jl:338)
+
+"""A mechanism compiled on the host (tables, species names, molecular weights, initial coverages)
+and its device-resident copy on one GPU (br_mech)."""
+mutable struct DeviceMech
+    host::Ptr{Cvoid}                   # br_host_mech (owns the br_mech_desc arrays)
+    m::Ptr{Cvoid}                      # br_mech on `device`
+    device::Int
+    ng::Int; ns::Int; nrg::Int; nrs::Int
+    species::Vector{String}            # gas species (mechanism order), then surface species
+    molwt::Vector{Float64}             # [ng] kg/mol
+    theta0::Vector{Float64}            # [ns]
+end
+ncomp(dm::DeviceMech) = dm.ng + dm.ns
+gas_species(dm::DeviceMech) = dm.species[1:dm.ng]
+surf_species(dm::DeviceMech) = dm.species[dm.ng+1:end]
+
+function _free!(dm::DeviceMech)
+    dm.m != C_NULL && ccall((:br_mech_destroy, lib), Cint, (Ptr{Cvoid},), dm.m)
+    dm.host != C_NULL && ccall((:br_host_mech_free, lib), Cint, (Ptr{Cvoid},), dm.host)
+    dm.m = C_NULL
+    dm.host = C_NULL
+    return nothing
+end
+
+"""compile_gaschemistry + IdealGas.create_thermo + SurfaceReactions.compile_mech
+(src/BatchReactor.jl:242-287) through br_mech_parse, then br_mech_create on `device`.
+`gas_mech == ""`: surface-only run, gas species from `gasphase` (space-separated, the <gasphase> tag)."""
+function compile_mechanism(gas_mech::AbstractString, therm::AbstractString, surf_mech::AbstractString="";
+                           gasphase::AbstractString="", conv::Integer=CONV_REFERENCE, device::Integer=0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:br_mech_parse, lib), Cint, (Cstring, Cstring, Cstring, Cstring, Cint, Ref{Ptr{Cvoid}}),
+                gas_mech, therm, surf_mech, gasphase, conv, h))
+    d = Ref{BrMechDesc}()
+    check(ccall((:br_host_mech_desc, lib), Cint, (Ptr{Cvoid}, Ref{BrMechDesc}), h[], d))
+    ng, ns, nrg, nrs = Int(d[].ng), Int(d[].ns), Int(d[].nrg), Int(d[].nrs)
+    buf = zeros(UInt8, 64)
+    names = String[]
+    for i in 0:(ng + ns - 1)
+        check(ccall((:br_host_mech_species, lib), Cint, (Ptr{Cvoid}, Cint, Ptr{UInt8}, Csize_t), h[], i, buf, 64))
+        push!(names, unsafe_string(pointer(buf)))
+    end
+    molwt = copy(unsafe_wrap(Array, d[].molwt, ng))
+    theta0 = zeros(ns)
+    check(ccall((:br_host_mech_theta0, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], theta0))
+    m = mech_create(d, device)
+    dm = DeviceMech(h[], m, Int(device), ng, ns, nrg, nrs, names, molwt, theta0)
+    finalizer(_free!, dm)
+    return dm
+end
+
+# br_batch_input (br_read_batch_xml)
+const BATCH_MAXCOMP = 64
+struct BrBatchInput
+    gas_mech::NTuple{256,UInt8}
+    surface_mech::NTuple{256,UInt8}
+    gasphase::NTuple{1024,UInt8}
+    T::Float64; p::Float64; Asv::Float64; time::Float64
+    has_T::Cint; has_p::Cint; has_Asv::Cint; has_time::Cint
+    ncomp::Cint; comp_is_mass::Cint
+    comp_names::NTuple{BATCH_MAXCOMP,NTuple{32,UInt8}}
+    comp_values::NTuple{BATCH_MAXCOMP,Float64}
+end
+function _cstr(t)
+    v = collect(t)
+    k = findfirst(==(0x00), v)
+    return String(v[1:(k === nothing ? length(v) : k - 1)])
+end
+
+"""input_data's view of batch.xml (src/BatchReactor.jl:238-306): a missing <Asv> reads as 1."""
+function read_batch_xml(path::AbstractString)
+    b = Ref{BrBatchInput}()
+    check(ccall((:br_read_batch_xml, lib), Cint, (Cstring, Ref{BrBatchInput}), path, b))
+    x = b[]
+    comp = Dict{String,Float64}(_cstr(x.comp_names[i]) => x.comp_values[i] for i in 1:Int(x.ncomp))
+    return (gas_mech=_cstr(x.gas_mech), surface_mech=_cstr(x.surface_mech), gasphase=_cstr(x.gasphase),
+            T=x.T, p=x.p, Asv=x.Asv, time=x.time, comp=comp, comp_is_mass=x.comp_is_mass != 0)
+end
+
+"""get_solution_vector (src/BatchReactor.jl:224-232): u0 = [rho*Y_k ; theta0] from mole (or mass)
+fractions by species name; rho0 = p Mbar / (R T)."""
+function initial_state(dm::DeviceMech, T::Real, p::Real, comp::AbstractDict; is_mass::Bool=false,
+                       theta::Union{Nothing,AbstractVector}=nothing)
+    ng = dm.ng
+    v = zeros(ng)
+    for (k, val) in comp
+        i = findfirst(==(uppercase(String(k))), gas_species(dm))
+        i === nothing && continue
+        v[i] = val
+    end
+    x = is_mass ? (t = v ./ dm.molwt; t ./ sum(t)) : v
+    Mb = sum(x .* dm.molwt)
+    rho = p * Mb / (R_GAS * T)
+    u = zeros(ncomp(dm))
+    u[1:ng] .= (x .* dm.molwt ./ Mb) .* rho
+    u[ng+1:end] .= theta === nothing ? dm.theta0 : theta
+    return u
+end
+
+"""Final conversion (src/BatchReactor.jl:142-144): Y = u / sum(u) over the gas species -> x."""
+function state_to_molefrac(dm::DeviceMech, u::AbstractVector)
+    y = u[1:dm.ng] ./ sum(u[1:dm.ng])
+    t = y ./ dm.molwt
+    return t ./ sum(t)
+end
+
+ignition_species(dm::DeviceMech) = something(findfirst(==("OH"), gas_species(dm)), 0)
+
+# ---- save_data (src/BatchReactor.jl:383-402): RxnHelperUtils' .dat (%10s / %.4e, TAB) and .csv
+#      (string(::Float64)) rows; x, p and coverages of the step's last RHS evaluation, rho from u
+function _write_profiles(folder, dm::DeviceMech, surf::Bool, T, trace, nst)
+    n, ng = ncomp(dm), dm.ng
+    g_dat = open(joinpath(folder, "gas_profile.dat"), "w")
+    s_dat = open(joinpath(folder, "surface_covg.dat"), "w")
+    g_csv = open(joinpath(folder, "gas_profile.csv"), "w")
+    s_csv = open(joinpath(folder, "surface_covg.csv"), "w")
+    try
+        hdr = vcat(["t", "T", "p", "rho"], gas_species(dm))
+        write(g_dat, join([@sprintf("%10s\t", h) for h in hdr]), "\n")
+        write(g_csv, join(hdr, ","), "\n")
+        if surf
+            sh = vcat(["t", "T"], surf_species(dm))
+            write(s_dat, join([@sprintf("%10s\t", h) for h in sh]), "\n")
+            write(s_csv, join(sh, ","), "\n")
+        end
+        for k in 0:nst
+            row = trace[:, k + 1, 1]
+            u, y = row[5:4+n], row[5+n:4+2n]
+            vals = vcat([row[1], T, row[4], sum(u[1:ng])], state_to_molefrac(dm, y))
+            write(g_dat, join([@sprintf("%.4e\t", v) for v in vals]), "\n")
+            write(g_csv, join(string.(vals), ","), "\n")
+            if surf
+                sv = vcat([row[1], T], y[ng+1:n])
+                write(s_dat, join([@sprintf("%.4e\t", v) for v in sv]), "\n")
+                write(s_csv, join(string.(sv), ","), "\n")
+            end
+        end
+    finally
+        close(g_dat); close(s_dat); close(g_csv); close(s_csv)
+    end
+end
+
+"""batch_reactor(input_file, lib_dir; sens, surfchem, gaschem) (src/BatchReactor.jl:67-70,:152-217)
+on the HIP engine: reads batch.xml, compiles the mechanism library files natively, integrates the
+reactor (CVODE_BDF restatement, rtol 1e-6, atol 1e-10), writes gas_profile.{dat,csv} and
+surface_covg.{dat,csv} next to the input and returns Symbol(retcode). sens=true returns
+(params, prob, t_span) with prob.f = residual! evaluated on the GPU (br_rhs)."""
+function batch_reactor(input_file::AbstractString, lib_dir::AbstractString; sens::Bool=false,
+                       surfchem::Bool=false, gaschem::Bool=false, device::Integer=0,
+                       conv::Integer=CONV_REFERENCE, max_steps::Integer=100_000)
+    inp = read_batch_xml(input_file)
+    gm = gaschem ? joinpath(lib_dir, inp.gas_mech) : ""
+    sm = surfchem ? joinpath(lib_dir, inp.surface_mech) : ""
+    dm = compile_mechanism(gm, joinpath(lib_dir, "therm.dat"), sm; gasphase=gaschem ? "" : inp.gasphase,
+                           conv=conv, device=device)
+    u0 = initial_state(dm, inp.T, inp.p, inp.comp; is_mass=inp.comp_is_mass)
+    n = ncomp(dm)
+    if sens
+        residual! = (du, u, p, t) -> (du .= rhs(dm, inp.T, inp.Asv, u); nothing)
+        params = (thermo=dm, cp=(Asv=inp.Asv, T=inp.T), chem=(surfchem=surfchem, gaschem=gaschem))
+        t_span = (0.0, inp.time)
+        return params, (f=residual!, u0=u0, tspan=t_span, p=params), t_span
+    end
+    opts = BrOpts(max_steps=max_steps, ignition_species=ignition_species(dm))
+    cap = min(4096, max_steps)
+    stats, trace = integrate_traced!(dm.m, [inp.T], [inp.Asv], reshape(copy(u0), n, 1), [inp.time]; cap=cap, opts=opts)
+    nst = Int(stats[1, 1])
+    if nst > cap   # deterministic: the repeat takes the same steps
+        stats, trace = integrate_traced!(dm.m, [inp.T], [inp.Asv], reshape(copy(u0), n, 1), [inp.time]; cap=nst,
+                                         opts=opts)
+        nst = Int(stats[1, 1])
+    end
+    _write_profiles(dirname(abspath(input_file)), dm, surfchem, inp.T, trace, nst)
+    _free!(dm)
+    return stats[8, 1] == 0 ? Symbol("Success") : Symbol("Failure")
+end
+
+"""residual!(du, u, p, t) (src/BatchReactor.jl:312-376) of one reactor on the GPU (br_rhs)."""
+function rhs(dm::DeviceMech, T::Real, Asv::Real, u::AbstractVector)
+    du = zeros(length(u))
+    check(ccall((:br_rhs, lib), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                dm.m, 1, [Float64(T)], [Float64(Asv)], collect(Float64, u), du))
+    return du
+end
+
+"""batch_reactor(inlet_comp, T, p, time; Asv, chem, thermo_obj, md) (src/BatchReactor.jl:86-147):
+returns (t = [0, time], Dict(species => x_end)); the mechanism is a DeviceMech from compile_mechanism."""
+function batch_reactor(inlet_comp::AbstractDict, T::Real, p::Real, time::Real; Asv::Real=1.0, md::DeviceMech)
+    u = reshape(initial_state(md, T, p, inlet_comp), ncomp(md), 1)
+    stats = integrate!(md.m, [Float64(T)], [Float64(Asv)], u, [Float64(time)])
+    stats[8, 1] == 0 || error("integration failed with status $(stats[8, 1])")
+    xf = state_to_molefrac(md, u[:, 1])
+    return [0.0, Float64(time)], Dict(zip(gas_species(md), xf))
+end
+
+"""batch_reactor_ensemble: N independent reactors, each with its own T, p, inlet composition and
+end time, in one call (one br_integrate over the ensemble). Returns (x_end [ng x N], theta_end
+[ns x N], stats [NSTAT x N], including t_ign from the OH marker)."""
+function batch_reactor_ensemble(md::DeviceMech, T::AbstractVector, p::AbstractVector, comps::AbstractVector,
+                                tf; Asv=1.0, rtol::Real=1e-6, atol::Real=1e-10)
+    N = length(T)
+    U = zeros(ncomp(md), N)
+    for i in 1:N
+        U[:, i] = initial_state(md, T[i], p[i], comps[i])
+    end
+    fillv(v) = v isa AbstractVector ? collect(Float64, v) : fill(Float64(v), N)
+    opts = BrOpts(rtol=rtol, atol=atol, ignition_species=ignition_species(md))
+    stats = integrate!(md.m, collect(Float64, T), fillv(Asv), U, fillv(tf); opts=opts)
+    X = reduce(hcat, [state_to_molefrac(md, U[:, i]) for i in 1:N])
+    return X, U[md.ng+1:end, :], stats
+end
+
 """The ensemble over several GPUs (br_integrate_multi): `mechs[d]` created on device d."""
 function integrate_multi!(mechs::Vector{Ptr{Cvoid}}, T, Asv, u::Matrix{Float64}, tf; opts::BrOpts=BrOpts())
     N = length(T)
@@ -107,5 +326,7 @@ function integrate_multi!(mechs::Vector{Ptr{Cvoid}}, T, Asv, u::Matrix{Float64},
                  Ptr{Float64}), mechs, length(mechs), N, T, Asv, u, tf, Ref(opts), stats))
     return stats
 end
+
+export batch_reactor, batch_reactor_ensemble, compile_mechanism, read_batch_xml, DeviceMech
 
 end # module

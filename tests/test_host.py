@@ -169,3 +169,103 @@ def test_reference_conventions_are_default(pkg, orc):
     m = pkg.Mechanism.from_files(LIB, gas_mech="grimech.dat")
     assert m.conv == pkg.CONV_REFERENCE == orc.CONV_REFERENCE == 19
     assert pkg.Mechanism.from_files(LIB, gas_mech="h2o2.dat", conv=0).conv == 0
+
+
+# --------------------------------------------------------------------------------------------
+# native (C++) mechanism compiler of libbrhip.so: br_mech_parse / br_read_batch_xml, the path a
+# Julia host uses (julia/BatchReactorHIP.jl) -- must give the Python compiler's tables bit for bit
+# --------------------------------------------------------------------------------------------
+_DESC_SHAPES = {  # field -> shape from (ng, ns, nrg, nrs)
+    "molwt": lambda g, s, r, q: (g,), "nasa": lambda g, s, r, q: (g, 15),
+    "g_nf": lambda g, s, r, q: (r,), "g_nr": lambda g, s, r, q: (r,), "g_f": lambda g, s, r, q: (r, 4),
+    "g_r": lambda g, s, r, q: (r, 4), "g_rev": lambda g, s, r, q: (r,), "g_tb": lambda g, s, r, q: (r,),
+    "g_arr": lambda g, s, r, q: (r, 3), "g_low": lambda g, s, r, q: (r, 3), "g_troe_n": lambda g, s, r, q: (r,),
+    "g_troe": lambda g, s, r, q: (r, 4), "g_eff": lambda g, s, r, q: (r, g), "sigma": lambda g, s, r, q: (s,),
+    "s_nf": lambda g, s, r, q: (q,), "s_np": lambda g, s, r, q: (q,), "s_f": lambda g, s, r, q: (q, 6),
+    "s_p": lambda g, s, r, q: (q, 6), "s_stick": lambda g, s, r, q: (q,), "s_arr": lambda g, s, r, q: (q, 3),
+    "s_ncov": lambda g, s, r, q: (q,), "s_cov_sp": lambda g, s, r, q: (q, 4), "s_cov_eps": lambda g, s, r, q: (q, 4),
+}
+
+
+def _native(pkg, gas=None, surf=None, gasphase=None, conv=None):
+    L = pkg._lib.lib()
+    h = ctypes.c_void_p()
+    enc = lambda s: None if s is None else s.encode()
+    rc = L.br_mech_parse(enc(gas and os.path.join(LIB, gas)), enc(os.path.join(LIB, "therm.dat")),
+                         enc(surf and os.path.join(LIB, surf)), enc(gasphase),
+                         pkg.CONV_REFERENCE if conv is None else conv, ctypes.byref(h))
+    if rc:
+        return rc, L.br_last_error().decode()
+    d = pkg._lib.MechDesc()
+    assert L.br_host_mech_desc(h, ctypes.byref(d)) == 0
+    sizes = (d.ng, d.ns, d.nrg, d.nrs)
+    out = {"sizes": sizes, "conv": d.conv, "p_std": d.p_std, "site_density": d.site_density}
+    for f, shp in _DESC_SHAPES.items():
+        s = shp(*sizes)
+        p = getattr(d, f)
+        out[f] = np.ctypeslib.as_array(p, shape=s).copy() if int(np.prod(s)) > 0 else None
+    buf = ctypes.create_string_buffer(64)
+    names = []
+    for i in range(d.ng + d.ns):
+        assert L.br_host_mech_species(h, i, buf, 64) == 0
+        names.append(buf.value.decode())
+    out["names"] = names
+    th = np.zeros(d.ns)
+    assert L.br_host_mech_theta0(h, pkg._lib.dptr(th)) == 0
+    out["theta0"] = th
+    assert L.br_host_mech_free(h) == 0
+    return 0, out
+
+
+@pytest.mark.parametrize("gas,surf,gasphase", [("grimech.dat", None, None), ("h2o2.dat", None, None),
+                                               (None, "ch4ni.xml", "CH4 H2O H2 CO CO2 O2 N2"),
+                                               ("grimech.dat", "ch4ni.xml", None)])
+def test_native_compiler_tables_bit_identical(pkg, gas, surf, gasphase):
+    """br_mech_parse (C++, libbrhip.so) builds the same br_mech_desc tables as the Python host
+    compiler, bit for bit (GRI, H2/O2, surface-only, gas + surface), with the same species order."""
+    rc, nat = _native(pkg, gas, surf, gasphase)
+    assert rc == 0, nat
+    m = pkg.Mechanism.from_files(LIB, gas_mech=gas, surface_mech=surf, gasphase=gasphase and gasphase.split())
+    assert nat["sizes"] == (m.ng, m.ns, m.nrg, m.nrs)
+    assert nat["names"] == m.species
+    assert nat["conv"] == m.conv and nat["p_std"] == m.p_std and nat["site_density"] == m.site_density
+    py = dict(m.tables, molwt=m.molwt, nasa=m.nasa, sigma=m.sigma)
+    for f in _DESC_SHAPES:
+        a, b = nat[f], np.asarray(py[f])
+        if a is None:
+            assert b.size == 0, f
+            continue
+        assert a.shape == b.shape, f
+        if a.dtype.kind == "f":
+            assert np.array_equal(a.view(np.uint64), np.ascontiguousarray(b, np.float64).view(np.uint64)), f
+        else:
+            assert np.array_equal(a, b), f
+    np.testing.assert_array_equal(nat["theta0"], m.theta0)
+
+
+def test_native_compiler_errors(pkg, tmp_path):
+    """Bad inputs come back as BR_ERR_INPUT with a message (no exception crosses the C-ABI)."""
+    rc, msg = _native(pkg, "nonexistent.dat")
+    assert rc == -10 and "cannot open" in msg
+    bad = tmp_path / "bad.dat"
+    bad.write_text("ELEMENTS H O END\nSPECIES H2 O2 END\nREACTIONS\nH2+XX=2H 1.0 0.0 0.0\nEND\n")
+    L = pkg._lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.br_mech_parse(str(bad).encode(), os.path.join(LIB, "therm.dat").encode(), None, None, 19, ctypes.byref(h))
+    assert rc == -10 and "unknown species 'XX'" in L.br_last_error().decode()
+
+
+@pytest.mark.parametrize("case", ["batch_h2o2", "batch_ch4", "batch_surf", "batch_gas_and_surf", "batch_udf"])
+def test_native_batch_xml(pkg, case):
+    """br_read_batch_xml reads the five reference scenario inputs as the Python reader does
+    (input_data, src/BatchReactor.jl:238-306); a missing <Asv> gives Asv = 1."""
+    path = os.path.join(GOLDEN, case, "batch.xml")
+    b = pkg._lib.BatchInput()
+    assert pkg._lib.lib().br_read_batch_xml(path.encode(), ctypes.byref(b)) == 0
+    d = pkg.read_batch_xml(path)
+    assert b.gas_mech.decode() == d.get("gas_mech", "") and b.surface_mech.decode() == d.get("surface_mech", "")
+    assert b.gasphase.decode().split() == d.get("gasphase", [])
+    assert (b.T, b.p, b.time) == (d["T"], d["p"], d["time"])
+    assert b.has_Asv == ("Asv" in d) and b.Asv == d.get("Asv", 1.0)
+    comp = {b.comp_names[i].value.decode(): b.comp_values[i] for i in range(b.ncomp)}
+    assert comp == d["molefractions"] and b.comp_is_mass == 0
