@@ -743,3 +743,26 @@ def test_integrate_multi_shards(pkg, gpu, ndev):
     assert np.array_equal(U1, Um) and np.array_equal(s1["yout"], sm["yout"])
     for k in ("nsteps", "nfe", "nje", "status", "t_ign"):
         assert np.array_equal(s1[k], sm[k]), k
+
+
+@pytest.mark.parametrize("scenario,flags,chem", [
+    ("batch_h2o2", ["--gas"], dict(gaschem=True)),
+    ("batch_surf", ["--surf"], dict(surfchem=True)),
+    ("batch_gas_and_surf", ["--gas", "--surf"], dict(gaschem=True, surfchem=True))])
+def test_native_cli_matches_python_host(pkg, gpu, tmp_path, scenario, flags, chem):
+    """The file-driven batch_reactor through the C-ABI only (brhip_batch: br_read_batch_xml,
+    br_mech_parse, br_mech_create, br_integrate_traced -- the Julia module's path, no Python in it)
+    writes the same four files as the Python host, byte for byte."""
+    import shutil
+    import subprocess
+    from conftest import GOLDEN, ROOT
+    a, b = tmp_path / "native", tmp_path / "python"
+    for d in (a, b):
+        d.mkdir()
+        shutil.copy(os.path.join(GOLDEN, scenario, "batch.xml"), d / "batch.xml")
+    cli = os.path.join(ROOT, "batchreactor.jl_amd", "brhip_batch")
+    r = subprocess.run([cli, str(a / "batch.xml"), LIB] + flags, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "Success", r.stderr
+    assert pkg.batch_reactor(str(b / "batch.xml"), LIB, **chem) == "Success"
+    for f in ("gas_profile.dat", "gas_profile.csv", "surface_covg.dat", "surface_covg.csv"):
+        assert (a / f).read_text() == (b / f).read_text(), f

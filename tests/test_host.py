@@ -269,3 +269,16 @@ def test_native_batch_xml(pkg, case):
     assert b.has_Asv == ("Asv" in d) and b.Asv == d.get("Asv", 1.0)
     comp = {b.comp_names[i].value.decode(): b.comp_values[i] for i in range(b.ncomp)}
     assert comp == d["molefractions"] and b.comp_is_mass == 0
+
+
+def test_cli_julia_string_format(pkg):
+    """brhip_batch (the C-ABI-only batch_reactor program) formats CSV numbers as Julia's
+    string(::Float64): every number token of the reference's own gas+surf CSVs comes back verbatim."""
+    import csv
+    toks = []
+    for name in ("gas_and_surf_golden.csv", "gas_and_surf_covg_golden.csv"):
+        for r in list(csv.reader(open(os.path.join(GOLDEN, name))))[1:]:
+            toks += r[1:]
+    cli = os.path.join(ROOT, "batchreactor.jl_amd", "brhip_batch")
+    out = subprocess.run([cli, "--fmt"], input="\n".join(toks), capture_output=True, text=True, check=True).stdout.split()
+    assert out == toks
