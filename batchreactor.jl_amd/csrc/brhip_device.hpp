@@ -969,7 +969,8 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
 // physical row swaps during the factorization (see LUWs for the stored form).
 // Pivot search on the bit patterns of |a_ik| (monotone for non-negative doubles): a 32-bit
 // DPP max over the high words, a second pass over the low words only when the high words tie,
-// then the lowest candidate lane holding the max (ballot + ff1) = the first max in row order.
+// then, among candidates holding the max, the one with the lowest ORIGINAL row index = the first
+// max in row order (the rows sit in lanes in the previous factorization's pivot order, lu_factor).
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned wave_umax(unsigned x) {
     x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
@@ -980,7 +981,8 @@ __device__ __forceinline__ unsigned wave_umax(unsigned x) {
     const unsigned r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
     return max(max(r0, r1), max(r2, r3));
 }
-__device__ __forceinline__ int pivot_lane(double v, bool cand) {   // v = |a_ik| on candidate rows
+// v = |a_ik| on candidate rows, prow = original row index held by this lane
+__device__ __forceinline__ int pivot_lane(double v, bool cand, int prow) {
     const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
     const unsigned hi = cand ? (unsigned)(bits >> 32) : 0u;
     const unsigned mh = wave_umax(hi);
@@ -989,7 +991,13 @@ __device__ __forceinline__ int pivot_lane(double v, bool cand) {   // v = |a_ik|
     if (__builtin_popcountll(m) > 1) {
         const unsigned lo = top ? (unsigned)bits : 0u;
         const unsigned ml = wave_umax(lo);
-        m = __ballot(top && lo == ml);
+        const bool top2 = top && lo == ml;
+        m = __ballot(top2);
+        if (__builtin_popcountll(m) > 1) {   // an exact tie: the first in original row order
+            const unsigned key = top2 ? ~(unsigned)prow : 0u;
+            const unsigned mk = wave_umax(key);
+            m = __ballot(top2 && key == mk);
+        }
     }
     return m ? (int)__builtin_ctzll(m) : 0;
 }
@@ -1009,17 +1017,17 @@ typedef __attribute__((address_space(3))) double LDSd;
 typedef __attribute__((address_space(3))) int LDSi;
 
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
-// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane =
-// original row), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
+// entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane = the
+// row it holds), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
 // Live columns go in chunks of 8 (measured round 1: 4: 63.9k, 2: 62.8k, 8: 64.1k GRI reactors/s).
 template <int W>
-__device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int& pstep,
+__device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int prow, int& pstep,
                                             double& dinv, int& fail, const LUWs& F) {
     constexpr int CH = 8;   // live-column granularity of the rank-1 update
     static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
-        const int p = pivot_lane(fabs(a[0]), pstep < 0);
+        const int p = pivot_lane(fabs(a[0]), pstep < 0, prow);
         const double piv = bcast(a[0], p);
         if (piv == 0.0 && !fail) fail = k + 1;
         const double rinv = 1.0 / piv;
@@ -1061,11 +1069,18 @@ __device__ __forceinline__ double lane_pull(double v, int src) {
 // 1 (left-looking: multipliers re-read from M, masked to rows not yet pivoted at that step;
 // pivot-row values broadcast from the panel-2 registers of the pivot lane, in step order), then
 // is factored right-looking. The arithmetic is exactly that of the unblocked right-looking LU.
-// Finally the rows of M are permuted into step order in place (gather, then store), and D^-1
-// is stored in step order. Returns 0 or k+1 for a zero pivot; *perm_out = pivot_perm.
+// The rows are loaded into the lanes in the previous factorization's pivot order (perm_io: lane s
+// holds original row perm_io[s]; the identity for a reactor's first LU): the rows of a stiff system
+// keep their pivot order from one Newton matrix to the next, so every step's pivot then sits on
+// the lane of its step, the factor matrix M comes out in pivot-step order as it is written, and
+// the gather pass (a read and a write of the whole matrix, ~9 MB per GRI reactor) is skipped.
+// Otherwise the rows of M are gathered into step order (in place) as before. D^-1 is stored in
+// step order. Row placement does not change the arithmetic: each row gets the same FMAs, and ties
+// in the pivot search go to the lowest original row. Returns 0 or k+1 for a zero pivot; perm_io:
+// step s -> original row on return.
 template <int NMAX>
 __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* __restrict__ ws, double gamma, int n,
-                                         int lane, int& perm_out) {
+                                         int lane, int& perm_io) {
     constexpr int P = NMAX < 32 ? NMAX : 32;
     constexpr int W2 = NMAX - P > 0 ? NMAX - P : 8;
     constexpr int CH = 8;
@@ -1074,6 +1089,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     BR_GLOBAL double* wsg = launder(ws);
     const LUWs F{wsg, wsg + NMAX * WAVE};
     lane = launder_v(lane);
+    const int prow = launder_v(perm_io);      // original row held by this lane (lanes >= n: lane)
     const bool act = lane < n;
     int pstep = act ? -1 : 1024;
     double dinv = 0.0;
@@ -1084,10 +1100,10 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         double a[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            const double jv = (j < n && act) ? J[j * WAVE + lane] : 0.0;
-            a[j] = ((j == lane) ? 1.0 : 0.0) - gamma * jv;
+            const double jv = (j < n && act) ? J[j * WAVE + prow] : 0.0;
+            a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
         }
-        lu_rl_steps<P>(a, 0, n1, n1, lane, pstep, dinv, fail, F);
+        lu_rl_steps<P>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, F);
     }
     BR_SUB_ADD(0, lt0);
     BR_SUB_T(lt1);
@@ -1096,8 +1112,8 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #pragma unroll
         for (int j = 0; j < W2; ++j) {
             const int col = P + j;
-            const double jv = (col < n && act) ? J[col * WAVE + lane] : 0.0;
-            b[j] = ((col == lane) ? 1.0 : 0.0) - gamma * jv;
+            const double jv = (col < n && act) ? J[col * WAVE + prow] : 0.0;
+            b[j] = ((col == prow) ? 1.0 : 0.0) - gamma * jv;
         }
         // multipliers of panel 1 re-read from M, one chunk of CH steps ahead
         double cur[CH], nxt[CH];
@@ -1121,19 +1137,26 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #pragma unroll
             for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
         }
-        lu_rl_steps<W2>(b, P, n, n, lane, pstep, dinv, fail, F);
+        lu_rl_steps<W2>(b, P, n, n, lane, prow, pstep, dinv, fail, F);
     }
     BR_SUB_ADD(1, lt1);
     BR_SUB_T(lt2);
-    // rows into step order, in place: chunk c is gathered completely before it is stored, and
-    // the gathers of chunk c+1 are in flight while chunk c is stored (columns >= n: zeros)
-    const int perm = pivot_perm(pstep, lane, n);
-    {
-        constexpr int NC = NMAX / CH;
+    constexpr int NC = NMAX / CH;
+    int perm;
+    if (__ballot(act && pstep != lane) == 0) {
+        // pivots in lane order: M is in step order already; padding columns n..NMAX-1 are zeros
+        perm = prow;
+        for (int c = n; c < NMAX; ++c) F.M[c * WAVE + lane] = 0.0;
+        F.D[lane] = dinv;
+    } else {
+        // rows into step order, in place: chunk c is gathered completely before it is stored, and
+        // the gathers of chunk c+1 are in flight while chunk c is stored (columns >= n: zeros)
+        const int q = pivot_perm(pstep, lane, n);   // lane holding the row of step `lane`
+        perm = __builtin_amdgcn_ds_bpermute(q * 4, prow);
         double g[2][CH];
         auto gather = [&](double (&v)[CH], int c) {
 #pragma unroll
-            for (int i = 0; i < CH; ++i) v[i] = F.M[min(c + i, n - 1) * WAVE + perm];
+            for (int i = 0; i < CH; ++i) v[i] = F.M[min(c + i, n - 1) * WAVE + q];
         };
         gather(g[0], 0);
 #pragma unroll
@@ -1144,10 +1167,10 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * WAVE + lane] = (t * CH + i < n) ? g[t & 1][i] : 0.0;
             __builtin_amdgcn_sched_barrier(0);
         }
+        F.D[lane] = lane_pull(dinv, q);
     }
-    F.D[lane] = lane_pull(dinv, perm);
     BR_SUB_ADD(2, lt2);
-    perm_out = perm;
+    perm_io = perm;
     return fail;
 }
 
