@@ -1116,6 +1116,29 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
             }
             BR_ACC(cyc_sol, c0);
         }
+#ifdef BR_EXP_VALU   // experiment: BR_EXP_VALU independent dummy fp64 FMAs per Newton iteration
+        {
+            double acc[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { acc[i] = delta[0] + i; asm volatile("" : "+v"(acc[i])); }
+#pragma unroll
+            for (int i = 0; i < BR_EXP_VALU / 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(acc[j]));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(acc[i]));
+        }
+#endif
+#ifdef BR_EXP_MEM   // experiment: BR_EXP_MEM columns (512 B each) of the saved J re-read per Newton iteration
+        {
+            const BR_GLOBAL double* jg = launder((const double*)Jsave);
+            double d[BR_EXP_MEM];
+#pragma unroll
+            for (int i = 0; i < BR_EXP_MEM; ++i) d[i] = jg[i * VW + lane];
+#pragma unroll
+            for (int i = 0; i < BR_EXP_MEM; ++i) asm volatile("" :: "v"(d[i]));
+        }
+#endif
         BR_CLK(c3);
         act_code = ctl_post_solve<CPL>(C, V, lane, delta, lu_fail);
         BR_ACC(cyc_ctl, c3);

@@ -972,14 +972,26 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
 // then, among candidates holding the max, the one with the lowest ORIGINAL row index = the first
 // max in row order (the rows sit in lanes in the previous factorization's pivot order, lu_factor).
 // ------------------------------------------------------------------------------------
+#ifndef BR_UMAX_BCAST
+#define BR_UMAX_BCAST 1
+#endif
 __device__ __forceinline__ unsigned wave_umax(unsigned x) {
     x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
     x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));
     x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));
     x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
+#if BR_UMAX_BCAST
+    // every lane holds its row's max: row_bcast:15 carries row r's into row r + 1 (rows 1, 3),
+    // row_bcast:31 row 1's into rows 2 and 3, so lane 63 ends with the wave max (2 DPP ops and
+    // one readlane instead of 4 readlanes and 3 maxes)
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xC, 0xF, false));
+    return __builtin_amdgcn_readlane(x, 63);
+#else
     const unsigned r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
     const unsigned r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
     return max(max(r0, r1), max(r2, r3));
+#endif
 }
 // v = |a_ik| on candidate rows, prow = original row index held by this lane
 __device__ __forceinline__ int pivot_lane(double v, bool cand, int prow) {
@@ -1019,11 +1031,18 @@ typedef __attribute__((address_space(3))) int LDSi;
 // right-looking steps k0..k1-1 on a left-aligned row segment a[0..W-1] (a[0] = column k0 on
 // entry) whose columns end at `cend`: pivot search on a[0], column k of the factors (lane = the
 // row it holds), rank-1 update of the live columns, shift by one (the k-loop stays rolled).
-// Live columns go in chunks of 8 (measured round 1: 4: 63.9k, 2: 62.8k, 8: 64.1k GRI reactors/s).
+// Live columns go in chunks of BR_LU_CH (round 3: 4 instead of 8 = -61k VALU instructions per GRI
+// reactor, +0.4 %; bit-identical).
+#ifndef BR_LU_CH
+#define BR_LU_CH 4
+#endif
+#ifndef BR_LL_SKIP
+#define BR_LL_SKIP 1
+#endif
 template <int W>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int prow, int& pstep,
                                             double& dinv, int& fail, const LUWs& F) {
-    constexpr int CH = 8;   // live-column granularity of the rank-1 update
+    constexpr int CH = BR_LU_CH;   // live-column granularity of the rank-1 update
     static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
@@ -1132,7 +1151,8 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
                 const int p = (int)__builtin_ctzll(m);
                 const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
 #pragma unroll
-                for (int j = 0; j < W2; ++j) b[j] = fma(-bcast_lu(b[j], p), l, b[j]);
+                for (int j = 0; j < W2; ++j)   // (padding columns P + j >= n skipped: uniform branch)
+                    if (!BR_LL_SKIP || j + 8 < W2 || P + j < n) b[j] = fma(-bcast_lu(b[j], p), l, b[j]);
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
