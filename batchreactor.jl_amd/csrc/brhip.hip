@@ -141,9 +141,16 @@ __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { retu
 // matrix columns hold 64 * CPL rows (CPL = 2 for nmax > 64)
 __host__ __device__ inline int col_rows(int nmax) { return nmax > 64 ? 128 : 64; }
 __host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * col_rows(nmax); }   // M, D
-// [J | LU factors | Jacobian scratch (2 per gas reaction) | RXD: {kf, kr} per gas reaction]
+// [J | LU factors, aliased by the Jacobian scratch (2 per gas reaction) | RXD: {kf, kr} per gas
+// reaction]. The scratch is live only while a new J is built, and every new J is followed by a
+// factorization that overwrites the old factors, so the two share one region (-5.2 KB per GRI
+// slot: 4096 slots of 63 KB = 258 MB instead of 280 MB against the 256 MB Infinity Cache).
+__host__ __device__ inline size_t lu_area_doubles(int nmax, int nrg) {
+    const size_t a = lu_ws_doubles(nmax), b = (((size_t)2 * nrg + 63) / 64) * 64;
+    return a > b ? a : b;
+}
 __host__ __device__ inline size_t rxd_ws_off(int nmax, int nrg) {
-    return (size_t)nmax * col_rows(nmax) + lu_ws_doubles(nmax) + (((size_t)2 * nrg + 63) / 64) * 64;
+    return (size_t)nmax * col_rows(nmax) + lu_area_doubles(nmax, nrg);
 }
 __host__ __device__ inline size_t ws_doubles(int nmax, int nrg) {
     return rxd_ws_off(nmax, nrg) + (((size_t)2 * nrg + 63) / 64) * 64;
@@ -992,7 +999,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
     double* Jsave = Jws + (size_t)widx * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
     double* LUsave = Jsave + NMAX * VW;
-    double* jscr = LUsave + lu_ws_doubles(NMAX);
+    double* jscr = LUsave;   // (aliases the factors: see rxd_ws_off)
     C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
     C->a_max_steps = o.max_steps; C->a_trace_cap = o.trace_cap; C->a_trace = trace; C->a_rid = rid; C->a_n = n;
     C->a_ign = o.ign; C->a_nout = o.nout; C->a_tout = o.tout; C->a_yout = o.yout;
@@ -1081,6 +1088,10 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         {
             BR_CLK(c0);
             rhs<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, p_last, f);
+#if defined(BR_EXP_DUP) && BR_EXP_DUP == 1   // experiment: the RHS twice (phase instruction counts)
+            asm volatile("" ::: "memory");
+            rhs<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, p_last, f);
+#endif
             BR_ACC(cyc_rhs, c0);
         }
         double b[CPL];
@@ -1096,6 +1107,10 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
             if (ui(C->newj)) {
                 BR_CLK(c0);
                 jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
+#if defined(BR_EXP_DUP) && BR_EXP_DUP == 3   // experiment: the Jacobian twice
+                asm volatile("" ::: "memory");
+                jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
+#endif
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
@@ -1109,6 +1124,14 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         if (!lu_fail) {
             BR_CLK(c0);
             if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
+#if defined(BR_EXP_DUP) && BR_EXP_DUP == 2   // experiment: the solve twice
+            if constexpr (CPL == 1) {
+                asm volatile("" ::: "memory");
+                double d2 = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
+                asm volatile("" : "+v"(d2));
+                delta[0] = d2;
+            }
+#endif
             else {
                 lu_solve2<NMAX>(LUsave, scr, n, lane, perm, b);
                 delta[0] = b[0];
@@ -1249,7 +1272,7 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
 #pragma unroll
     FOR_S u[s] = CS < M.n ? U[(size_t)rid * M.n + CS] : 0.0;
     double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);
-    jacobian<CPL>(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * VW + lu_ws_doubles(NMAX));
+    jacobian<CPL>(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * VW);
 #pragma unroll
     FOR_S {
         if (CS < M.n) {

@@ -1021,6 +1021,17 @@ __device__ __forceinline__ int pivot_lane(double v, bool cand, int prow) {
 // (A packed-triangle layout -- each sweep reading one triangle front to back, 25.5 KB instead of
 // ~29 KB per GRI solve from the fabric -- measured 2.7 % slower in round 3: its column segments
 // start at arbitrary 8-B offsets, so every load instruction spans one more 128-B line.)
+// saved-J loads of the LU (each line read once per factorization): optionally non-temporal
+#ifndef BR_LU_NT
+#define BR_LU_NT 0
+#endif
+__device__ __forceinline__ double ldj(const BR_GLOBAL double* p) {
+#if BR_LU_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 struct LUWs {
     BR_GLOBAL double* M;
     BR_GLOBAL double* D;
@@ -1119,7 +1130,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         double a[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            const double jv = (j < n && act) ? J[j * WAVE + prow] : 0.0;
+            const double jv = (j < n && act) ? ldj(J + j * WAVE + prow) : 0.0;
             a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
         }
         lu_rl_steps<P>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, F);
@@ -1131,7 +1142,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #pragma unroll
         for (int j = 0; j < W2; ++j) {
             const int col = P + j;
-            const double jv = (col < n && act) ? J[col * WAVE + prow] : 0.0;
+            const double jv = (col < n && act) ? ldj(J + col * WAVE + prow) : 0.0;
             b[j] = ((col == prow) ? 1.0 : 0.0) - gamma * jv;
         }
         // multipliers of panel 1 re-read from M, one chunk of CH steps ahead
@@ -1239,13 +1250,19 @@ __device__ __forceinline__ void dpp_off(double& r, double x, const double (&v)[1
 // shares a 128-B line with the rows that do update except at 3 line boundaries. Raw buffer
 // loads: per-lane offset in the VGPR (one v_max / v_min per column), the chunk's column base
 // c * 512 B in soffset and the column within the chunk as the immediate (<= 3584 B).
+// cache policy of the solve's factor loads (aux bits of the buffer load: 2 = nt, streaming). A
+// factor line is re-read only by the wave's next solve, ~60k cycles later, after the XCD's other
+// 511 waves have streamed ~17 MB through its 4 MB L2: it never survives there.
+#ifndef BR_SOLVE_AUX
+#define BR_SOLVE_AUX 0
+#endif
 template <bool FWD>
 __device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned lane8) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const unsigned k8 = (unsigned)(c + i) * 8u;
         const unsigned off = FWD ? max(lane8, k8) : min(lane8, k8);
-        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (WAVE * 8), c * (WAVE * 8), 0));
+        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (WAVE * 8), c * (WAVE * 8), BR_SOLVE_AUX));
     }
 }
 // block T of a sweep (blocks of 16 columns, the last one NMAX % 16 wide if that is not 0),
@@ -1511,11 +1528,11 @@ __device__ __forceinline__ void tri2_load_blk(double (&v0)[16], double (&v1)[16]
             const int cb = (c0 + i) * 128 * 8;
             if (want0) {
                 const unsigned o0 = FWD ? max(lane8, k8) : min(lane8, k8);
-                v0[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, 0));
+                v0[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, BR_SOLVE_AUX));
             }
             if (want1) {
                 const unsigned o1 = FWD ? min(max(hi8, k8), 79u * 8u) : min(hi8, k8);
-                v1[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, cb, 0));
+                v1[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, cb, BR_SOLVE_AUX));
             }
         }
     }
