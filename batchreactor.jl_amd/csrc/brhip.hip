@@ -91,28 +91,27 @@ struct Ctl {
 };
 constexpr int CTL_BYTES = (sizeof(Ctl) + 15) / 16 * 16;
 enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, acor, ewt, tempv, y
-// V[vec * VW + component], VW = 64 * CPL components per vector
-// Two components per lane (n = 65..72): the vectors are stored 72 wide, not 128; components
-// 72..127 (lanes 8..63 of the second slot, never active) share one 56-double dump row, so a
-// gas+surface reactor needs 5.7 KB instead of 9.2 KB here (8 reactors per CU instead of 6)
-constexpr int VROW2 = 72;
-__host__ __device__ inline int vec_bytes(int cpl) { return cpl == 2 ? (NVEC * VROW2 + 64) * 8 : NVEC * WAVE * 8; }
+// V[vec * 64 + lane] for the first component slot. Two components per lane (n = 65..72): slot 1 of
+// vector j (components 64..71, lanes 0..7) at V1OFF + 8 j + lane; lanes 8..63 of slot 1 (components
+// 72..127, never real) at V1OFF + 8 j + 72 + lane, a dump region whose entries alias only each other.
+// Every access is then base + per-lane constant + 8 j (an immediate): no per-vector select that
+// the compiler would hoist out of the integrator loop and keep live (40 VGPRs spilled at 3 waves/
+// SIMD with the previous 72-wide rows and one shared dump row). 6.6 KB per gas+surface reactor.
+constexpr int V1OFF = NVEC * 64;
+__host__ __device__ inline int vec_bytes(int cpl) {
+    return cpl == 2 ? (V1OFF + 8 * (NVEC - 1) + 72 + 64) * 8 : NVEC * WAVE * 8;
+}
 // Nordsieck / work vectors in the reactor's LDS block: V.at(vec, s) = component lane + 64 s of
 // vector vec. (Register-resident vectors stored to LDS around each Newton setup measured GRI
 // -1.1 %, surf -11 % in round 2: the extra VGPRs cost occupancy.)
 template <int CPL>
-struct VA {   // LDS rows (VW = 64 * CPL components per vector; CPL = 2 rows are 72 wide, see VROW2)
+struct VA {
     typedef __attribute__((address_space(3))) double LD;
     LD* p;
     int lane;
     __device__ __forceinline__ LD& at(int j, int s) const {
-        const int i = j * 64 * CPL + lane + 64 * s;
-        if constexpr (CPL == 1) {
-            return p[i];
-        } else {
-            const int row = i >> 7, c = i & 127;
-            return c < VROW2 ? p[row * VROW2 + c] : p[NVEC * VROW2 + (c & 63)];
-        }
+        if (CPL == 1 || s == 0) return p[j * 64 + lane];
+        return p[V1OFF + 8 * j + (lane < 8 ? lane : 72 + lane)];
     }
 };
 template <int CPL> using VT = VA<CPL>;
@@ -139,7 +138,7 @@ __host__ __device__ inline size_t reactor_bytes(const DevMech& M) {
 __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return M.img_bytes + rpb * reactor_bytes(M); }
 // per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn);
 // matrix columns hold 64 * CPL rows (CPL = 2 for nmax > 64)
-__host__ __device__ inline int col_rows(int nmax) { return nmax > 64 ? 128 : 64; }
+__host__ __device__ inline int col_rows(int nmax) { return nmax > 64 ? CR2 : 64; }   // CR2 = 80 (lu_factor2)
 __host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * col_rows(nmax); }   // M, D
 // [J | LU factors, aliased by the Jacobian scratch (2 per gas reaction) | RXD: {kf, kr} per gas
 // reaction]. The scratch is live only while a new J is built, and every new J is followed by a
@@ -943,7 +942,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
 #define BR_MAXRPB56 16   // n in 33..64: one workgroup of up to 16 reactors per CU (tables staged once)
 #endif
 #ifndef BR_MAXRPB72
-#define BR_MAXRPB72 8   // n > 64 (gas + surface): one workgroup of up to 8 reactors per CU (tables staged once)
+#define BR_MAXRPB72 12   // n > 64 (gas + surface): one workgroup of up to 12 reactors per CU (tables staged once)
 #endif
 __host__ __device__ constexpr int br_maxrpb(int nmax) {
     return nmax > 64 ? BR_MAXRPB72 : (nmax == 56 || nmax == 64) ? BR_MAXRPB56 : 4;
@@ -954,7 +953,7 @@ constexpr size_t LDS_PER_CU = 160 * 1024, LDS_GRANULE = 1280;   // gfx950 (granu
 #endif
 // minimum waves per SIMD the register allocator must allow, per instance
 #ifndef BR_WPE72
-#define BR_WPE72 2   // n > 64: 2 waves/SIMD
+#define BR_WPE72 3   // n > 64: 3 waves/SIMD (168 VGPRs, 26 spilled; 11 reactors per CU by LDS: +3 % over 2 waves)
 #endif
 #ifndef BR_WPE56
 #define BR_WPE56 4   // n in 33..64 (GRI): 4 waves/SIMD (<= 128 VGPRs; 16 x 8.8 KB + tables fit the LDS)
@@ -968,7 +967,6 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const double* __restrict__ tfv, KOpts o, double* __restrict__ stats, double* __restrict__ Jws,
     double* __restrict__ trace) {
     constexpr int CPL = NMAX > 64 ? 2 : 1;   // components per lane
-    constexpr int VW = 64 * CPL;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const WaveCtx W = wave_ctx<CPL, NMAX>(M, smem_raw, rpb, Jws);
     // Reactor indices: with o.work every wave of the (resident-sized) grid keeps taking the next
@@ -998,7 +996,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const double Asv = Asvv ? Asvv[rid] : 1.0;
     const double Asv_th = (M.conv & 4) ? 1.0 : Asv;
     double* Jsave = Jws + (size_t)widx * ws_doubles(NMAX, M.nrg);   // J, LU factors, Jacobian scratch
-    double* LUsave = Jsave + NMAX * VW;
+    double* LUsave = Jsave + NMAX * col_rows(NMAX);
     double* jscr = LUsave;   // (aliases the factors: see rxd_ws_off)
     C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
     C->a_max_steps = o.max_steps; C->a_trace_cap = o.trace_cap; C->a_trace = trace; C->a_rid = rid; C->a_n = n;
@@ -1157,7 +1155,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
             const BR_GLOBAL double* jg = launder((const double*)Jsave);
             double d[BR_EXP_MEM];
 #pragma unroll
-            for (int i = 0; i < BR_EXP_MEM; ++i) d[i] = jg[i * VW + lane];
+            for (int i = 0; i < BR_EXP_MEM; ++i) d[i] = jg[i * 64 * CPL + lane];
 #pragma unroll
             for (int i = 0; i < BR_EXP_MEM; ++i) asm volatile("" :: "v"(d[i]));
         }
@@ -1257,7 +1255,7 @@ __global__ __launch_bounds__(256) void k_rhs(DevMech M, int N, int rpb, const do
 template <int NMAX>
 __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const double* Tv, const double* Asvv,
                                              const double* U, double* J, double* Jws) {
-    constexpr int CPL = NMAX > 64 ? 2 : 1, VW = 64 * CPL;
+    constexpr int CPL = NMAX > 64 ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const WaveCtx W = wave_ctx<CPL, NMAX>(M, smem_raw, rpb, Jws);
     const int rid = W.rid;
@@ -1272,12 +1270,12 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
 #pragma unroll
     FOR_S u[s] = CS < M.n ? U[(size_t)rid * M.n + CS] : 0.0;
     double* Jsave = Jws + (size_t)rid * ws_doubles(NMAX, M.nrg);
-    jacobian<CPL>(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * VW);
+    jacobian<CPL>(M, W.tb, S, T, Asv, Asv_th, u, lane, Jsave, Jsave + NMAX * col_rows(NMAX));
 #pragma unroll
     FOR_S {
         if (CS < M.n) {
             double* row = J + ((size_t)rid * M.n + CS) * M.n;
-            for (int j = 0; j < M.n; ++j) row[j] = Jsave[j * VW + CS];
+            for (int j = 0; j < M.n; ++j) row[j] = Jsave[j * col_rows(NMAX) + CS];
         }
     }
 }
@@ -2089,8 +2087,8 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
 template <int NMAX>
 __global__ __launch_bounds__(64) void k_lu_check2(int N, int n, const double* J, const double* g, const double* b,
                                                   double* x, double* ws, int* fail) {
-    constexpr int JW = 128;
-    __shared__ double scr[192];
+    constexpr int JW = CR2;
+    __shared__ double scr[256];
     const int rid = blockIdx.x;
     if (rid >= N) return;
     const int lane = threadIdx.x;
@@ -2099,7 +2097,7 @@ __global__ __launch_bounds__(64) void k_lu_check2(int N, int n, const double* J,
     for (int j = 0; j < NMAX; ++j)
         for (int s = 0; s < 2; ++s) {
             const int row = lane + 64 * s;
-            Jt[j * JW + row] = (row < n && j < n) ? J[((size_t)rid * n + row) * n + j] : 0.0;
+            if (row < JW) Jt[j * JW + row] = (row < n && j < n) ? J[((size_t)rid * n + row) * n + j] : 0.0;
         }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();

@@ -743,7 +743,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                                          double Asv_th, const double (&u)[CPL], int lane, double* Jsave_,
                                          double* jscr_) {
     typedef Lay<CPL> L;
-    constexpr int JW = 64 * CPL;   // Jacobian column stride
+    constexpr int JW = CPL == 2 ? 80 : 64;   // Jacobian column stride (CPL = 2: CR2 rows, see lu_factor2)
     BR_GLOBAL double* Jsave = launder(Jsave_);
     BR_GLOBAL double* jscr = launder(jscr_);
     const Tab tb = tab_view<CPL>(br_lds, M);
@@ -957,7 +957,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
             double v;
             if (k < MF(ng)) v = (j < MF(ng) ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * sf;
             else v = Asv_th * tb.sigma[k] / MF(G) * sf;
-            Jsave[j * JW + k] = act ? v : 0.0;
+            if (k < JW) Jsave[j * JW + k] = act ? v : 0.0;
         }
         wave_sync();
     }
@@ -1328,36 +1328,54 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
 }
 
 // ------------------------------------------------------------------------------------
-// 64 < n <= 128 (CPL = 2): lane holds rows lane and lane + 64. Same factorization semantics
-// (first max |a_ik| in row order, same multipliers and update order); column stride 128; the
-// panels are 16 columns wide (registers: 2 x 16 per lane); the inverse permutation and the
-// row gathers of P b and D^-1 go through LDS scratch (>= 192 doubles) instead of ds_permute.
+// 64 < n <= 72 (CPL = 2): lane holds positions lane and lane + 64. Same factorization semantics
+// (first max |a_ik| in original row order, same multipliers and update order). Columns hold
+// CR2 = 80 rows (5 lines: positions 64..79 are lanes 0..15 of the second slot; lanes 16..63 there
+// never hold a row and never touch memory), not 128 (round 3: 37.5 % fewer bytes per factor and
+// J column written). As for CPL = 1 the rows are loaded in the previous factorization's pivot
+// order (prow: position -> original row), so when every pivot lands on its own position the
+// factors are already in step order and the gather pass is skipped. The panels are 16 columns
+// wide (registers: 2 x 16 per lane); the inverse permutation, P b and D^-1 go through LDS scratch
+// (>= 256 doubles).
 // ------------------------------------------------------------------------------------
+constexpr int CR2 = 80;
 
-__device__ __forceinline__ int pivot_row2(double v0, bool c0, double v1, bool c1) {
+// first max |a| over candidate positions; exact ties go to the lowest ORIGINAL row (prow)
+__device__ __forceinline__ int pivot_row2(double v0, bool c0, double v1, bool c1, const int (&prow)[2]) {
     const unsigned long long b0 = (unsigned long long)__double_as_longlong(v0);
     const unsigned long long b1 = (unsigned long long)__double_as_longlong(v1);
     const unsigned h0 = c0 ? (unsigned)(b0 >> 32) : 0u, h1 = c1 ? (unsigned)(b1 >> 32) : 0u;
     const unsigned mh = wave_umax(max(h0, h1));
-    const bool t0 = c0 && h0 == mh, t1 = c1 && h1 == mh;
+    bool t0 = c0 && h0 == mh, t1 = c1 && h1 == mh;
     unsigned long long m0 = __ballot(t0), m1 = __ballot(t1);
     if (__builtin_popcountll(m0) + __builtin_popcountll(m1) > 1) {
         const unsigned l0 = t0 ? (unsigned)b0 : 0u, l1 = t1 ? (unsigned)b1 : 0u;
         const unsigned ml = wave_umax(max(l0, l1));
-        m0 = __ballot(t0 && l0 == ml);
-        m1 = __ballot(t1 && l1 == ml);
+        t0 = t0 && l0 == ml;
+        t1 = t1 && l1 == ml;
+        m0 = __ballot(t0);
+        m1 = __ballot(t1);
+        if (__builtin_popcountll(m0) + __builtin_popcountll(m1) > 1) {   // exact tie: lowest original row
+            const unsigned k0 = t0 ? ~(unsigned)prow[0] : 0u, k1 = t1 ? ~(unsigned)prow[1] : 0u;
+            const unsigned mk = wave_umax(max(k0, k1));
+            m0 = __ballot(t0 && k0 == mk);
+            m1 = __ballot(t1 && k1 == mk);
+        }
     }
     return m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : 0);
 }
 
 template <int W>
 __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, int cend, int lane, int (&pstep)[2],
-                                             double (&dinv)[2], int& fail, const LUWs& F) {
-    constexpr int CH = 8, JW = 128;
+                                             double (&dinv)[2], int& fail, const LUWs& F, const int (&prow)[2]) {
+    constexpr int CH = 8;
     static_assert(W % CH == 0, "W must be a multiple of 8");
+    // the second slot's lanes 16..63 (positions 80..127, never rows) all address row 79: every
+    // value they hold or write there is 0 (padding rows), so no memory op needs an exec mask
+    const int o1 = min(64 + lane, CR2 - 1);
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
-        const int pr = pivot_row2(fabs(a[0][0]), pstep[0] < 0, fabs(a[1][0]), pstep[1] < 0);
+        const int pr = pivot_row2(fabs(a[0][0]), pstep[0] < 0, fabs(a[1][0]), pstep[1] < 0, prow);
         const int p = pr & 63, ps = pr >> 6;
         const double piv = ps ? bcast(a[1][0], p) : bcast(a[0][0], p);
         if (piv == 0.0 && !fail) fail = k + 1;
@@ -1368,7 +1386,7 @@ __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, 
             const bool isp = (ps == s) && (lane == p);
             const bool rem = (pstep[s] < 0) && !isp;
             l[s] = rem ? a[s][0] * rinv : 0.0;
-            F.M[k * JW + 64 * s + lane] = rem ? l[s] : ((pstep[s] >= 0) ? a[s][0] * dinv[s] : 0.0);
+            F.M[k * CR2 + (s ? o1 : lane)] = rem ? l[s] : ((pstep[s] >= 0) ? a[s][0] * dinv[s] : 0.0);
             if (isp) { pstep[s] = k; dinv[s] = rinv; }
         }
         const int live = cend - k;
@@ -1397,34 +1415,35 @@ __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, 
     }
 }
 
-// one 16-column panel starting at column C0: load, left-looking updates by steps 0..C0-1
-// (multipliers from M in original row order, masked to rows not yet pivoted at that step),
-// right-looking factorization of its own columns; then the next panel
+// one 16-column panel starting at column C0: load (rows in prow order), left-looking updates by
+// steps 0..C0-1 (multipliers from M in position order, masked to positions not yet pivoted at
+// that step), right-looking factorization of its own columns; then the next panel
 template <int NMAX, int C0>
 __device__ __forceinline__ void lu2_panels(const BR_GLOBAL double* J, double gamma, int n, int lane, int (&pstep)[2],
-                                           double (&dinv)[2], int& fail, const LUWs& F) {
+                                           double (&dinv)[2], int& fail, const LUWs& F, const int (&prow)[2]) {
     if constexpr (C0 < NMAX) {
-        constexpr int JW = 128, W = (NMAX - C0) < 16 ? (NMAX - C0) : 16;
+        constexpr int W = (NMAX - C0) < 16 ? (NMAX - C0) : 16;
         if (C0 < n) {
+            const int o1 = min(64 + lane, CR2 - 1);   // (see lu_rl_steps2)
             double a[2][W];
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const int row = lane + 64 * s;
+                const int row = prow[s];
 #pragma unroll
                 for (int j = 0; j < W; ++j) {
                     const int col = C0 + j;
-                    const double jv = (col < n && row < n) ? J[col * JW + row] : 0.0;
+                    const double jv = (col < n && row < n) ? J[col * CR2 + row] : 0.0;
                     a[s][j] = ((col == row) ? 1.0 : 0.0) - gamma * jv;
                 }
             }
             if (C0 > 0) {
-                double n0 = F.M[lane], n1 = F.M[64 + lane];
+                double n0 = F.M[lane], n1 = F.M[o1];
 #pragma unroll 1
                 for (int k = 0; k < C0; ++k) {
                     const double m0 = n0, m1 = n1;
                     const int kn = (k + 1 < C0) ? k + 1 : k;
-                    n0 = F.M[kn * JW + lane];
-                    n1 = F.M[kn * JW + 64 + lane];
+                    n0 = F.M[kn * CR2 + lane];
+                    n1 = F.M[kn * CR2 + o1];
                     const unsigned long long b0 = __ballot(pstep[0] == k), b1 = __ballot(pstep[1] == k);
                     const int p = b0 ? (int)__builtin_ctzll(b0) : (int)__builtin_ctzll(b1);
                     const double l0 = ((unsigned)pstep[0] > (unsigned)k) ? m0 : 0.0;
@@ -1443,52 +1462,76 @@ __device__ __forceinline__ void lu2_panels(const BR_GLOBAL double* J, double gam
                 }
             }
             const int kend = (C0 + W < n) ? C0 + W : n;
-            lu_rl_steps2<W>(a, C0, kend, kend, lane, pstep, dinv, fail, F);
+            lu_rl_steps2<W>(a, C0, kend, kend, lane, pstep, dinv, fail, F, prow);
         }
-        lu2_panels<NMAX, C0 + 16>(J, gamma, n, lane, pstep, dinv, fail, F);
+        lu2_panels<NMAX, C0 + 16>(J, gamma, n, lane, pstep, dinv, fail, F, prow);
     }
 }
 
+// perm_io[s]: on entry the original row loaded into position lane + 64 s (the previous
+// factorization's step -> row map; identity for a reactor's first LU), on return this one's.
 template <int NMAX>
 __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double* __restrict__ ws, LDSd* scr,
-                                          double gamma, int n, int lane, int (&perm_out)[2]) {
-    constexpr int JW = 128, CH = 4, NC = NMAX / CH;
-    static_assert(NMAX % 8 == 0 && NMAX <= 128, "NMAX");
+                                          double gamma, int n, int lane, int (&perm_io)[2]) {
+    constexpr int CH = 4, NC = NMAX / CH;
+    static_assert(NMAX % 8 == 0 && NMAX <= CR2 && NMAX > 64, "NMAX");
     const BR_GLOBAL double* J = launder(J_);
     BR_GLOBAL double* wsg = launder(ws);
-    const LUWs F{wsg, wsg + NMAX * JW};
+    const LUWs F{wsg, wsg + NMAX * CR2};
     lane = launder_v(lane);
-    int pstep[2];
+    int pstep[2], prow[2];
     double dinv[2] = {0.0, 0.0};
     int fail = 0;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) pstep[s] = (lane + 64 * s < n) ? -1 : 1024;
-    lu2_panels<NMAX, 0>(J, gamma, n, lane, pstep, dinv, fail, F);
-    // inverse permutation through LDS: step s <- row perm[s] (rows >= n map to themselves)
-    LDSi* isc = (LDSi*)scr;
-    LDSd* dsc = scr + 64;
+    for (int s = 0; s < 2; ++s) {
+        const int pos = lane + 64 * s;
+        prow[s] = (pos < n) ? launder_v(perm_io[s]) : pos;
+        pstep[s] = (pos < n) ? -1 : 1024;
+    }
+    lu2_panels<NMAX, 0>(J, gamma, n, lane, pstep, dinv, fail, F, prow);
+    const int o1 = min(64 + lane, CR2 - 1);   // (see lu_rl_steps2)
+    if (__ballot((lane < n && pstep[0] != lane) || (lane + 64 < n && pstep[1] != lane + 64)) == 0) {
+        // every pivot on its own position: M is in step order already; D^-1 in step order
+        F.D[lane] = dinv[0];
+        F.D[o1] = dinv[1];
+        for (int c = n; c < NMAX; ++c) {
+            F.M[c * CR2 + lane] = 0.0;
+            F.M[c * CR2 + o1] = 0.0;
+        }
+        perm_io[0] = prow[0];
+        perm_io[1] = prow[1];
+        return fail;
+    }
+    // inverse permutation through LDS: position of step s (positions >= n map to themselves),
+    // and the original row / D^-1 of every position
+    LDSi* isc = (LDSi*)scr;            // [128] step -> position
+    LDSi* rsc = (LDSi*)(scr + 64);     // [128] position -> original row
+    LDSd* dsc = scr + 128;             // [128] position -> D^-1
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        const int row = lane + 64 * s;
-        isc[(row < n) ? pstep[s] : row] = row;
-        dsc[row] = dinv[s];
+        const int pos = lane + 64 * s;
+        isc[(pos < n) ? pstep[s] : pos] = pos;
+        rsc[pos] = prow[s];
+        dsc[pos] = dinv[s];
     }
     wave_sync();
-    int perm[2];
+    int q[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        perm[s] = isc[lane + 64 * s];
-        F.D[64 * s + lane] = dsc[perm[s]];
+        q[s] = isc[lane + 64 * s];
+        perm_io[s] = rsc[q[s]];
     }
+    F.D[lane] = dsc[q[0]];
+    F.D[o1] = dsc[q[1]];
     wave_sync();
-    // rows into step order, in place, chunks of CH columns double-buffered (columns >= n: zeros)
+    // positions into step order, in place, chunks of CH columns double-buffered (columns >= n: zeros)
     double g[2][2][CH];
     auto gather = [&](double (&v)[2][CH], int c) {
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
             const int col = (c + i < n) ? c + i : n - 1;
-            v[0][i] = F.M[col * JW + perm[0]];
-            v[1][i] = F.M[col * JW + perm[1]];
+            v[0][i] = F.M[col * CR2 + q[0]];
+            v[1][i] = F.M[col * CR2 + min(q[1], CR2 - 1)];
         }
     };
     gather(g[0], 0);
@@ -1499,13 +1542,11 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
             const int col = t * CH + i;
-            F.M[col * JW + lane] = (col < n) ? g[t & 1][0][i] : 0.0;
-            F.M[col * JW + 64 + lane] = (col < n) ? g[t & 1][1][i] : 0.0;
+            F.M[col * CR2 + lane] = (col < n) ? g[t & 1][0][i] : 0.0;
+            F.M[col * CR2 + o1] = (col < n) ? g[t & 1][1][i] : 0.0;
         }
         __builtin_amdgcn_sched_barrier(0);
     }
-    perm_out[0] = perm[0];
-    perm_out[1] = perm[1];
     return fail;
 }
 
@@ -1525,7 +1566,7 @@ __device__ __forceinline__ void tri2_load_blk(double (&v0)[16], double (&v1)[16]
     for (int i = 0; i < 16; ++i) {
         if (i < CW) {
             const unsigned k8 = (unsigned)(c0 + i) * 8u;
-            const int cb = (c0 + i) * 128 * 8;
+            const int cb = (c0 + i) * CR2 * 8;
             if (want0) {
                 const unsigned o0 = FWD ? max(lane8, k8) : min(lane8, k8);
                 v0[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, BR_SOLVE_AUX));
@@ -1544,16 +1585,18 @@ __device__ __forceinline__ void tri_sweeps2_dpp(__amdgpu_buffer_rsrc_t rs, int l
     constexpr int W1 = NMAX - 64;
     const unsigned lane8 = (unsigned)lane * 8u, hi8 = lane8 + 512u;
     const int xl = lane & 15;
-    double v[2][2][16];
+    // slot-0 factors double-buffered (the next block's in flight during this one), slot-1 factors
+    // (rows 64..79) loaded at the start of their own block and consumed after its diagonal part:
+    // 96 instead of 128 VGPRs of buffers (the kernel's peak; 3 waves/SIMD need <= 168)
+    double v0[2][16], v1[16];
     // ---- forward: blocks 0..3 (r0), then block 4 (r1)
-    tri2_load_blk<true, 16>(v[0][0], v[0][1], rs, 0, lane8, hi8, true, true);
+    tri2_load_blk<true, 16>(v0[0], v1, rs, 0, lane8, hi8, true, false);
     auto fwd_blk = [&](auto B_) {
         constexpr int B = decltype(B_)::value;
-        double (&f0)[16] = v[B & 1][0];
-        double (&f1)[16] = v[B & 1][1];
+        double (&f0)[16] = v0[B & 1];
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (B < 3) tri2_load_blk<true, 16>(v[(B + 1) & 1][0], v[(B + 1) & 1][1], rs, 16 * (B + 1), lane8, hi8, true, true);
-        else tri2_load_blk<true, W1>(v[(B + 1) & 1][0], v[(B + 1) & 1][1], rs, 64, lane8, hi8, false, true);
+        tri2_load_blk<true, 16>(v0[B & 1], v1, rs, 16 * B, lane8, hi8, false, true);
+        if constexpr (B < 3) tri2_load_blk<true, 16>(v0[(B + 1) & 1], v1, rs, 16 * (B + 1), lane8, hi8, true, false);
         __builtin_amdgcn_sched_barrier(0);
         dpp_diag<true, 16, 1 << B, 0>(r[0], f0);
         asm volatile("s_nop 1");
@@ -1561,36 +1604,37 @@ __device__ __forceinline__ void tri_sweeps2_dpp(__amdgpu_buffer_rsrc_t rs, int l
         wave_sync();
         const double x = x64[16 * B + xl];
         if constexpr (B < 3) dpp_off<true, 16, (0xF << (B + 1)) & 0xF, 0>(r[0], x, f0);
-        dpp_off<true, 16, 0x1, 0>(r[1], x, f1);
+        dpp_off<true, 16, 0x1, 0>(r[1], x, v1);
         wave_sync();
     };
     fwd_blk(std::integral_constant<int, 0>{});
     fwd_blk(std::integral_constant<int, 1>{});
     fwd_blk(std::integral_constant<int, 2>{});
     fwd_blk(std::integral_constant<int, 3>{});
-    dpp_diag<true, W1, 0x1, 0>(r[1], v[0][1]);          // block 4 (buffer 4 & 1 = 0)
+    tri2_load_blk<true, W1>(v0[0], v1, rs, 64, lane8, hi8, false, true);
+    dpp_diag<true, W1, 0x1, 0>(r[1], v1);               // block 4
     asm volatile("s_nop 1");
     r[0] *= dv[0];
     r[1] *= dv[1];
     // ---- backward: block 4 (r1) first, then blocks 3..0 (r0)
-    tri2_load_blk<false, W1>(v[0][0], v[0][1], rs, 64, lane8, hi8, true, true);
+    tri2_load_blk<false, W1>(v0[0], v1, rs, 64, lane8, hi8, true, true);
     __builtin_amdgcn_sched_barrier(0);
-    tri2_load_blk<false, 16>(v[1][0], v[1][1], rs, 48, lane8, hi8, true, false);
+    tri2_load_blk<false, 16>(v0[1], v1, rs, 48, lane8, hi8, true, false);
     __builtin_amdgcn_sched_barrier(0);
-    dpp_diag<false, W1, 0x1, 0>(r[1], v[0][1]);
+    dpp_diag<false, W1, 0x1, 0>(r[1], v1);
     asm volatile("s_nop 1");
     x64[lane] = r[1];
     wave_sync();
     {
         const double x = x64[xl];
-        dpp_off<false, W1, 0xF, 0>(r[0], x, v[0][0]);
+        dpp_off<false, W1, 0xF, 0>(r[0], x, v0[0]);
     }
     wave_sync();
     auto bwd_blk = [&](auto B_, auto BUF_) {
         constexpr int B = decltype(B_)::value, BUF = decltype(BUF_)::value;
-        double (&f0)[16] = v[BUF][0];
+        double (&f0)[16] = v0[BUF];
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (B > 0) tri2_load_blk<false, 16>(v[BUF ^ 1][0], v[BUF ^ 1][1], rs, 16 * (B - 1), lane8, hi8, true, false);
+        if constexpr (B > 0) tri2_load_blk<false, 16>(v0[BUF ^ 1], v1, rs, 16 * (B - 1), lane8, hi8, true, false);
         __builtin_amdgcn_sched_barrier(0);
         dpp_diag<false, 16, 1 << B, 0>(r[0], f0);
         if constexpr (B > 0) {
@@ -1612,10 +1656,9 @@ __device__ __forceinline__ void tri_sweeps2_dpp(__amdgpu_buffer_rsrc_t rs, int l
 template <int NMAX>
 __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* scr, int n, int lane,
                                           const int (&perm)[2], double (&b)[2]) {
-    constexpr int JW = 128;
     const BR_GLOBAL double* wsg = launder(ws);
     lane = launder_v(lane);
-    LDSd* dsc = scr + 64;
+    LDSd* dsc = scr + 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) dsc[lane + 64 * s] = (lane + 64 * s < n) ? b[s] : 0.0;
     wave_sync();
@@ -1625,10 +1668,10 @@ __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* s
     // (all solve loads are buffer loads: drain first so the waitcnt pass can count them in order)
     __builtin_amdgcn_s_waitcnt(0x70);
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * JW * 8, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * CR2 * 8, 0x00020000);
     const double dv[2] = {
-        __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * JW * 8, 0)),
-        __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8 + 512, NMAX * JW * 8, 0))};
+        __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * CR2 * 8, 0)),
+        __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, min(lane, CR2 - 65) * 8 + 512, NMAX * CR2 * 8, 0))};
     tri_sweeps2_dpp<NMAX>(rs, lane, r, dv, scr);
     b[0] = (lane < n) ? r[0] : 0.0;
     b[1] = (lane + 64 < n) ? r[1] : 0.0;
