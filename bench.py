@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-phase", action="store_true", help="skip the rate+Jacobian phase split (diag build)")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive extra step (counter runs: "
+                                                          "one integrator dispatch per timed step only)")
     ap.add_argument("--phase-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.phase_only:
@@ -140,10 +142,15 @@ def main():
     alg_bytes = N * 8.0 * ((3 + mech.n) + (mech.n + pkg._lib.NSTAT))
 
     # measured memory-side bytes per reactor of this kernel at this HEAD (rocprofv3 FETCH_SIZE x2
-    # + WRITE_SIZE passes, scripts/pmc_traffic.py -> profiles/r02_traffic_<config>.json)
+    # + WRITE_SIZE passes, scripts/pmc_traffic.py -> profiles/r03_traffic_<config>.json)
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", f"r02_traffic_{args.config}.json")
-    if os.path.exists(tpath):
+    tpath = None
+    for rnd in ("r03", "r02"):   # the newest round's summary
+        cand = os.path.join(ROOT, "profiles", f"{rnd}_traffic_{args.config}.json")
+        if os.path.exists(cand):
+            tpath = cand
+            break
+    if tpath:
         with open(tpath) as fh:
             tj = json.load(fh)
         traffic = tj["bytes_per_reactor"] * N
@@ -160,23 +167,9 @@ def main():
     # PCIe-inclusive rate (the integrate call including H2D/D2H): one more step with
     # the inputs in pinned host memory and the final states + counters copied back to it. Reported
     # beside `value` (which, per the bench contract, starts with the inputs resident in HBM).
-    hT, hA, hU0, htf = (torch.from_numpy(a).pin_memory() for a in (T, Asv, U0, tf))
-    hU = torch.empty_like(hU0).pin_memory()
-    hst = torch.empty(dst.shape, dtype=dst.dtype).pin_memory()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    p0 = time.perf_counter()
-    dT.copy_(hT, non_blocking=True); dA.copy_(hA, non_blocking=True); dtf.copy_(htf, non_blocking=True)
-    dU0.copy_(hU0, non_blocking=True)
-    step()
-    if world > 1:   # every rank receives the gathered ensemble
-        for t in gathered[0]:
-            t.cpu()
-    else:
-        hU.copy_(dU, non_blocking=True); hst.copy_(dst, non_blocking=True)
-    torch.cuda.synchronize()
-    pcie_s = shard.max_over_ranks(time.perf_counter() - p0, dist if world > 1 else None, dev)
+    pcie_s = None
+    if not args.no_pcie:
+        pcie_s = pcie_step(torch, dist, world, dev, (T, Asv, U0, tf), (dT, dA, dU0, dtf), dU, dst, step, gathered, shard)
 
     cpu = parity = phases = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -238,11 +231,34 @@ def main():
             "parity_vs_oracle": parity,
             "gather_ms": gather_ms,
             "gather_in_timed_region": world > 1,
-            "value_incl_h2d_d2h": ok_all / pcie_s,
+            "value_incl_h2d_d2h": (ok_all / pcie_s) if pcie_s else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pcie_step(torch, dist, world, dev, host_in, dev_in, dU, dst, step, gathered, shard):
+    """One more step with the inputs in pinned host memory and the final states + counters copied
+    back to it (PCIe-inclusive wall time, max over ranks)."""
+    hT, hA, hU0, htf = (torch.from_numpy(a).pin_memory() for a in host_in)
+    dT, dA, dU0, dtf = dev_in
+    hU = torch.empty_like(hU0).pin_memory()
+    hst = torch.empty(dst.shape, dtype=dst.dtype).pin_memory()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    p0 = time.perf_counter()
+    dT.copy_(hT, non_blocking=True); dA.copy_(hA, non_blocking=True); dtf.copy_(htf, non_blocking=True)
+    dU0.copy_(hU0, non_blocking=True)
+    step()
+    if world > 1:   # every rank receives the gathered ensemble
+        for t in gathered[0]:
+            t.cpu()
+    else:
+        hU.copy_(dU, non_blocking=True); hst.copy_(dst, non_blocking=True)
+    torch.cuda.synchronize()
+    return shard.max_over_ranks(time.perf_counter() - p0, dist if world > 1 else None, dev)
 
 
 def run_phase_split(config):

@@ -22,9 +22,9 @@ STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *prof* ]] && run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${PROF_ARGS:---steps 3 --warmup 1}
 if [[ $STEPS == *pmc* ]]; then   # HBM traffic of k_integrate: separate counter passes (no tracing)
   PN=${PMC_N:-20000}
-  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- python3 bench.py --no-cpu --no-phase --n $PN --steps 1 --warmup 0 ${PMC_ARGS:-}
-  run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- python3 bench.py --no-cpu --no-phase --n $PN --steps 1 --warmup 0 ${PMC_ARGS:-}
-  run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmc_t -o run -- python3 bench.py --no-cpu --no-phase --n $PN --steps 1 --warmup 0 ${PMC_ARGS:-}
+  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- python3 bench.py --no-cpu --no-phase --no-pcie --n $PN --steps 1 --warmup 0 ${PMC_ARGS:-}
+  run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- python3 bench.py --no-cpu --no-phase --no-pcie --n $PN --steps 1 --warmup 0 ${PMC_ARGS:-}
+  run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmc_t -o run -- python3 bench.py --no-cpu --no-phase --no-pcie --n $PN --steps 1 --warmup 0 ${PMC_ARGS:-}
   python3 scripts/pmc_traffic.py $(ls gpurun_out/pmc_f/*counter_collection.csv) $(ls gpurun_out/pmc_w/*counter_collection.csv) $PN gpurun_out/traffic_gri.json $(ls gpurun_out/pmc_t/*counter_collection.csv)
 fi
 echo done

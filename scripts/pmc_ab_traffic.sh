@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 C=${CFG:-gri}; N=${PMC_N:-20000}
-A="--no-cpu --no-phase --config $C --n $N --steps 1 --warmup 0"
+A="--no-cpu --no-phase --no-pcie --config $C --n $N --steps 1 --warmup 0"
 for v in "$@"; do
   lib=$PWD/batchreactor.jl_amd/libbrhip_$v.so; [ "$v" = cur ] && lib=$PWD/batchreactor.jl_amd/libbrhip.so
   rm -rf gpurun_out/ptf_$v gpurun_out/ptw_$v

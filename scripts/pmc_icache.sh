@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 C=${1:-gri}; N=${2:-20000}
-A="--no-cpu --no-phase --config $C --n $N --steps 1 --warmup 0"
+A="--no-cpu --no-phase --no-pcie --config $C --n $N --steps 1 --warmup 0"
 timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE --output-format csv -d gpurun_out/pmc_ic1_$C -o run -- python3 bench.py $A > gpurun_out/pmc_ic1_$C.log 2>&1 || { echo "pass 1 failed"; tail -5 gpurun_out/pmc_ic1_$C.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_IFETCH SQ_IFETCH_LEVEL SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d gpurun_out/pmc_ic2_$C -o run -- python3 bench.py $A > gpurun_out/pmc_ic2_$C.log 2>&1 || { echo "pass 2 failed"; tail -5 gpurun_out/pmc_ic2_$C.log; exit 1; }
 python3 - "$C" "$N" <<'PY'

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 C=${1:-gri}; N=${2:-20000}
-A="--no-cpu --no-phase --config $C --n $N --steps 1 --warmup 0"
+A="--no-cpu --no-phase --no-pcie --config $C --n $N --steps 1 --warmup 0"
 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_lat1_$C -o run -- python3 bench.py $A > gpurun_out/pmc_lat1_$C.log 2>&1 || { echo "pass 1 failed"; tail -5 gpurun_out/pmc_lat1_$C.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_sum TCC_CYCLE_sum --output-format csv -d gpurun_out/pmc_lat2_$C -o run -- python3 bench.py $A > gpurun_out/pmc_lat2_$C.log 2>&1 || { echo "pass 2 failed"; tail -5 gpurun_out/pmc_lat2_$C.log; exit 1; }
 python3 - "$C" <<'PY'

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 C=${1:-gri}; N=${2:-20000}
-A="--no-cpu --no-phase --config $C --n $N --steps 1 --warmup 0"
+A="--no-cpu --no-phase --no-pcie --config $C --n $N --steps 1 --warmup 0"
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_LDS_ATOMIC SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS --output-format csv -d gpurun_out/pmc_lds_$C -o run -- python3 bench.py $A > gpurun_out/pmc_lds_$C.log 2>&1 || { echo "pass failed"; tail -5 gpurun_out/pmc_lds_$C.log; exit 1; }
 python3 - "$C" "$N" <<'PY'
 import csv, glob, json, sys
