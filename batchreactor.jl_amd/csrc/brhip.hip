@@ -139,7 +139,10 @@ __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { retu
 // per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn);
 // matrix columns hold 64 * CPL rows (CPL = 2 for nmax > 64)
 __host__ __device__ inline int col_rows(int nmax) { return nmax > 64 ? CR2 : 64; }   // CR2 = 80 (lu_factor2)
-__host__ __device__ inline size_t lu_ws_doubles(int nmax) { return (size_t)(nmax + 1) * col_rows(nmax); }   // M, D
+// factors + D^-1: CPL = 1 NMAX columns of NMAX rows + 64 (lu_factor), CPL = 2 NMAX + 1 columns of CR2 rows
+__host__ __device__ inline size_t lu_ws_doubles(int nmax) {
+    return nmax > 64 ? (size_t)(nmax + 1) * CR2 : (size_t)nmax * nmax + WAVE;
+}
 // [J | LU factors, aliased by the Jacobian scratch (2 per gas reaction) | RXD: {kf, kr} per gas
 // reaction]. The scratch is live only while a new J is built, and every new J is followed by a
 // factorization that overwrites the old factors, so the two share one region (-5.2 KB per GRI

@@ -1013,8 +1013,8 @@ __device__ __forceinline__ int pivot_lane(double v, bool cand, int prow) {
     }
     return m ? (int)__builtin_ctzll(m) : 0;
 }
-// Factor workspace (global, per reactor): ONE combined factor matrix, column-major, 64 rows
-// per column, rows in pivot-step order after lu_factor returns: column k holds L[s][k] on rows
+// Factor workspace (global, per reactor): ONE combined factor matrix, column-major, NMAX rows
+// per column (round 3: 56 for GRI instead of 64: 12.5 % less factor footprint and solve traffic), rows in pivot-step order after lu_factor returns: column k holds L[s][k] on rows
 // s > k, U'[s][k] = (D^-1 U)[s][k] on rows s < k and 0 on s = k; then D^-1 in step order.
 // The forward sweep reads only rows below the diagonal and the backward sweep only rows above
 // it (exec-masked loads skip whole 128-B lines), so a solve moves ~n^2 doubles instead of 2*n*64.
@@ -1050,10 +1050,13 @@ typedef __attribute__((address_space(3))) int LDSi;
 #ifndef BR_LL_SKIP
 #define BR_LL_SKIP 1
 #endif
-template <int W>
+template <int W, int FR>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int prow, int& pstep,
                                             double& dinv, int& fail, const LUWs& F) {
     constexpr int CH = BR_LU_CH;   // live-column granularity of the rank-1 update
+    // factor columns hold FR = NMAX rows; lanes >= FR (never rows, their values are 0) store into the
+    // spare tail of the D^-1 vector, which is rewritten after the factorization
+    const int fo = (lane < FR) ? lane : (int)(F.D - F.M) + lane;
     static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
@@ -1064,7 +1067,7 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
         const bool isp = (lane == p);
         const bool rem = (pstep < 0) && !isp;
         const double l = rem ? a[0] * rinv : 0.0;
-        F.M[k * WAVE + lane] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
+        F.M[((lane < FR) ? k * FR : 0) + fo] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
         if (isp) { pstep = k; dinv = rinv; }
         const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
 #pragma unroll
@@ -1117,9 +1120,11 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     static_assert(NMAX % CH == 0 && NMAX <= 64, "lu_factor: NMAX");
     const BR_GLOBAL double* J = launder(J_);
     BR_GLOBAL double* wsg = launder(ws);
-    const LUWs F{wsg, wsg + NMAX * WAVE};
+    constexpr int FR = NMAX;   // factor column stride (rows): [M: NMAX columns of NMAX rows | D^-1: 64]
+    const LUWs F{wsg, wsg + NMAX * FR};
     lane = launder_v(lane);
     const int prow = launder_v(perm_io);      // original row held by this lane (lanes >= n: lane)
+    const int lc = min(lane, FR - 1);
     const bool act = lane < n;
     int pstep = act ? -1 : 1024;
     double dinv = 0.0;
@@ -1133,7 +1138,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (j < n && act) ? ldj(J + j * WAVE + prow) : 0.0;
             a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
         }
-        lu_rl_steps<P>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, F);
+        lu_rl_steps<P, FR>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, F);
     }
     BR_SUB_ADD(0, lt0);
     BR_SUB_T(lt1);
@@ -1148,12 +1153,12 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         // multipliers of panel 1 re-read from M, one chunk of CH steps ahead
         double cur[CH], nxt[CH];
 #pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = F.M[i * WAVE + lane];
+        for (int i = 0; i < CH; ++i) cur[i] = (lane < FR) ? F.M[i * FR + lc] : 0.0;
 #pragma unroll 1
         for (int kb = 0; kb < P; kb += CH) {
             if (kb + CH < P) {
 #pragma unroll
-                for (int i = 0; i < CH; ++i) nxt[i] = F.M[(kb + CH + i) * WAVE + lane];
+                for (int i = 0; i < CH; ++i) nxt[i] = (lane < FR) ? F.M[(kb + CH + i) * FR + lc] : 0.0;
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) {
@@ -1168,7 +1173,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #pragma unroll
             for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
         }
-        lu_rl_steps<W2>(b, P, n, n, lane, prow, pstep, dinv, fail, F);
+        lu_rl_steps<W2, FR>(b, P, n, n, lane, prow, pstep, dinv, fail, F);
     }
     BR_SUB_ADD(1, lt1);
     BR_SUB_T(lt2);
@@ -1177,7 +1182,8 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     if (__ballot(act && pstep != lane) == 0) {
         // pivots in lane order: M is in step order already; padding columns n..NMAX-1 are zeros
         perm = prow;
-        for (int c = n; c < NMAX; ++c) F.M[c * WAVE + lane] = 0.0;
+        if (lane < FR)
+            for (int c = n; c < NMAX; ++c) F.M[c * FR + lane] = 0.0;
         F.D[lane] = dinv;
     } else {
         // rows into step order, in place: chunk c is gathered completely before it is stored, and
@@ -1187,15 +1193,17 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         double g[2][CH];
         auto gather = [&](double (&v)[CH], int c) {
 #pragma unroll
-            for (int i = 0; i < CH; ++i) v[i] = F.M[min(c + i, n - 1) * WAVE + q];
+            for (int i = 0; i < CH; ++i) v[i] = F.M[min(c + i, n - 1) * FR + min(q, FR - 1)];
         };
         gather(g[0], 0);
 #pragma unroll
         for (int t = 0; t < NC; ++t) {
             if (t + 1 < NC) gather(g[(t + 1) & 1], (t + 1) * CH);
             __builtin_amdgcn_sched_barrier(0);
+            if (lane < FR) {
 #pragma unroll
-            for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * WAVE + lane] = (t * CH + i < n) ? g[t & 1][i] : 0.0;
+                for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * FR + lane] = (t * CH + i < n) ? g[t & 1][i] : 0.0;
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         F.D[lane] = lane_pull(dinv, q);
@@ -1256,27 +1264,28 @@ __device__ __forceinline__ void dpp_off(double& r, double x, const double (&v)[1
 #ifndef BR_SOLVE_AUX
 #define BR_SOLVE_AUX 0
 #endif
-template <bool FWD>
-__device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned lane8) {
+template <bool FWD, int FR>
+__device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned ld8) {
+    // ld8: the lane clamped to FR - 1 (lanes >= FR are never sources; they read row FR - 1)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const unsigned k8 = (unsigned)(c + i) * 8u;
-        const unsigned off = FWD ? max(lane8, k8) : min(lane8, k8);
-        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (WAVE * 8), c * (WAVE * 8), BR_SOLVE_AUX));
+        const unsigned off = FWD ? max(ld8, k8) : min(ld8, k8);
+        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (FR * 8), c * (FR * 8), BR_SOLVE_AUX));
     }
 }
 // block T of a sweep (blocks of 16 columns, the last one NMAX % 16 wide if that is not 0),
 // factor loads one block ahead; x64 = 64 doubles of LDS scratch
 template <bool FWD, int NMAX, int T>
-__device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigned lane8, double& r, LDSd* x64,
-                                              double (&v)[2][16]) {
+__device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigned lane8, unsigned ld8, double& r,
+                                              LDSd* x64, double (&v)[2][16]) {
     constexpr int NB = (NMAX + 15) / 16;
     if constexpr (T < NB) {
         constexpr int B = FWD ? T : NB - 1 - T;            // block = DPP row
         constexpr int CW = (16 * B + 16 > NMAX) ? NMAX - 16 * B : 16;
         auto load = [&](double (&d)[16], int blk) {
-            tri_load_diag<FWD>(*reinterpret_cast<double(*)[8]>(&d[0]), rs, 16 * blk, lane8);
-            if (16 * blk + 8 < NMAX) tri_load_diag<FWD>(*reinterpret_cast<double(*)[8]>(&d[8]), rs, 16 * blk + 8, lane8);
+            tri_load_diag<FWD, NMAX>(*reinterpret_cast<double(*)[8]>(&d[0]), rs, 16 * blk, ld8);
+            if (16 * blk + 8 < NMAX) tri_load_diag<FWD, NMAX>(*reinterpret_cast<double(*)[8]>(&d[8]), rs, 16 * blk + 8, ld8);
         };
         if constexpr (T == 0) load(v[0], B);
         __builtin_amdgcn_sched_barrier(0);
@@ -1293,13 +1302,13 @@ __device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigne
             dpp_off<FWD, CW, ROWS, 0>(r, x, f);
             wave_sync();
         }
-        tri_block_dpp<FWD, NMAX, T + 1>(rs, lane8, r, x64, v);
+        tri_block_dpp<FWD, NMAX, T + 1>(rs, lane8, ld8, r, x64, v);
     }
 }
 template <bool FWD, int NMAX>
 __device__ __forceinline__ void tri_sweep_dpp(__amdgpu_buffer_rsrc_t rs, int lane, double& r, LDSd* x64) {
     double v[2][16];
-    tri_block_dpp<FWD, NMAX, 0>(rs, (unsigned)lane * 8u, r, x64, v);
+    tri_block_dpp<FWD, NMAX, 0>(rs, (unsigned)lane * 8u, (unsigned)min(lane, NMAX - 1) * 8u, r, x64, v);
     asm volatile("s_nop 1");
 }
 
@@ -1318,8 +1327,8 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
     // controller would make the counter out of order too), so drain it first
     __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0)
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX + 1) * WAVE * 8, 0x00020000);
-    const double dinv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * WAVE * 8, 0));
+        __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX * NMAX + WAVE) * 8, 0x00020000);
+    const double dinv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * NMAX * 8, 0));
     double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
     tri_sweep_dpp<true, NMAX>(rs, lane, r, x16);
     r *= dinv;
