@@ -146,7 +146,7 @@ __host__ __device__ inline size_t lu_ws_doubles(int nmax) {
 // [J | LU factors, aliased by the Jacobian scratch (2 per gas reaction) | RXD: {kf, kr} per gas
 // reaction]. The scratch is live only while a new J is built, and every new J is followed by a
 // factorization that overwrites the old factors, so the two share one region (-5.2 KB per GRI
-// slot: 4096 slots of 63 KB = 258 MB instead of 280 MB against the 256 MB Infinity Cache).
+// slot; with NMAX-row factor columns 4096 slots of 60 KB = 245 MB against the 256 MB Infinity Cache).
 __host__ __device__ inline size_t lu_area_doubles(int nmax, int nrg) {
     const size_t a = lu_ws_doubles(nmax), b = (((size_t)2 * nrg + 63) / 64) * 64;
     return a > b ? a : b;
