@@ -972,35 +972,41 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
 // then, among candidates holding the max, the one with the lowest ORIGINAL row index = the first
 // max in row order (the rows sit in lanes in the previous factorization's pivot order, lu_factor).
 // ------------------------------------------------------------------------------------
-#ifndef BR_UMAX_BCAST
-#define BR_UMAX_BCAST 1
-#endif
+// Wave max of a 32-bit value: 4 DPP steps inside each 16-lane row, then row_bcast:15 carries row r's
+// max into row r + 1 (rows 1, 3) and row_bcast:31 row 1's into rows 2 and 3, so lane 63 holds the
+// wave max; each step is one v_max_u32_dpp (written as inline asm: the compiler split the two
+// row-masked steps into a v_mov, a v_mov_dpp and a v_max each). s_nop 1: the VALU-write ->
+// DPP-read hazard of each step, and the readlane after the last.
 __device__ __forceinline__ unsigned wave_umax(unsigned x) {
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
-#if BR_UMAX_BCAST
-    // every lane holds its row's max: row_bcast:15 carries row r's into row r + 1 (rows 1, 3),
-    // row_bcast:31 row 1's into rows 2 and 3, so lane 63 ends with the wave max (2 DPP ops and
-    // one readlane instead of 4 readlanes and 3 maxes)
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xA, 0xF, false));
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xC, 0xF, false));
-    return __builtin_amdgcn_readlane(x, 63);
-#else
-    const unsigned r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
-    const unsigned r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
-    return max(max(r0, r1), max(r2, r3));
-#endif
+    unsigned r;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "=&v"(r)
+        : "v"(x));
+    return __builtin_amdgcn_readlane(r, 63);
 }
-// v = |a_ik| on candidate rows, prow = original row index held by this lane
-__device__ __forceinline__ int pivot_lane(double v, bool cand, int prow) {
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
-    const unsigned hi = cand ? (unsigned)(bits >> 32) : 0u;
+// a = a_ik, cm = 0x7fffffff on candidate rows (not pivoted yet), 0 elsewhere; prow = original row
+// index held by this lane. hi = high word of |a_ik| on candidates, 0 elsewhere, so when the max is
+// not 0 the lanes holding it are candidates (one compare for the ballot).
+__device__ __forceinline__ int pivot_lane(double a, unsigned cm, int prow) {
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(a);
+    const unsigned hi = (unsigned)(bits >> 32) & cm;
     const unsigned mh = wave_umax(hi);
-    const bool top = cand && hi == mh;
-    unsigned long long m = __ballot(top);
+    unsigned long long m = (mh != 0) ? __ballot(hi == mh) : __ballot(cm != 0);
     if (__builtin_popcountll(m) > 1) {
+        const bool top = (mh != 0) ? (hi == mh) : (cm != 0);
         const unsigned lo = top ? (unsigned)bits : 0u;
         const unsigned ml = wave_umax(lo);
         const bool top2 = top && lo == ml;
@@ -1036,6 +1042,15 @@ struct LUWs {
     BR_GLOBAL double* M;
     BR_GLOBAL double* D;
 };
+// raw buffer ops over the CPL = 1 factor matrix: the column base goes in soffset (scalar), the
+// row in the per-lane offset; a lane that holds no row (lane >= FR) gets an out-of-range offset,
+// so the buffer range check drops its stores and returns 0 for its loads (no exec masks, no
+// address selects)
+constexpr unsigned LU_OOB = 0x80000000u;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lu_rsrc(BR_GLOBAL double* M, int doubles) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)M, (short)0, doubles * 8, 0x00020000);
+}
 typedef __attribute__((address_space(3))) double LDSd;
 typedef __attribute__((address_space(3))) int LDSi;
 
@@ -1047,27 +1062,25 @@ typedef __attribute__((address_space(3))) int LDSi;
 #ifndef BR_LU_CH
 #define BR_LU_CH 4
 #endif
-#ifndef BR_LL_SKIP
-#define BR_LL_SKIP 1
-#endif
 template <int W, int FR>
 __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int cend, int lane, int prow, int& pstep,
-                                            double& dinv, int& fail, const LUWs& F) {
+                                            double& dinv, int& fail, __amdgpu_buffer_rsrc_t rs) {
     constexpr int CH = BR_LU_CH;   // live-column granularity of the rank-1 update
-    // factor columns hold FR = NMAX rows; lanes >= FR (never rows, their values are 0) store into the
-    // spare tail of the D^-1 vector, which is rewritten after the factorization
-    const int fo = (lane < FR) ? lane : (int)(F.D - F.M) + lane;
+    // factor columns hold FR = NMAX rows (lanes >= FR never hold a row: their stores are dropped)
+    const unsigned fo8 = (lane < FR) ? (unsigned)lane * 8u : LU_OOB;
     static_assert(W % CH == 0, "W must be a multiple of the chunk");
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
-        const int p = pivot_lane(fabs(a[0]), pstep < 0, prow);
+        const bool cand = pstep < 0;
+        const int p = pivot_lane(a[0], cand ? 0x7fffffffu : 0u, prow);
         const double piv = bcast(a[0], p);
         if (piv == 0.0 && !fail) fail = k + 1;
         const double rinv = 1.0 / piv;
         const bool isp = (lane == p);
-        const bool rem = (pstep < 0) && !isp;
+        const bool rem = cand && !isp;
         const double l = rem ? a[0] * rinv : 0.0;
-        F.M[((lane < FR) ? k * FR : 0) + fo] = rem ? l : ((pstep >= 0) ? a[0] * dinv : 0.0);
+        const double fv = rem ? l : (cand ? 0.0 : a[0] * dinv);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fv), rs, fo8, k * (FR * 8), 0);
         if (isp) { pstep = k; dinv = rinv; }
         const int live = cend - k;              // columns k..cend-1 are live in a[0..live-1]
 #pragma unroll
@@ -1122,9 +1135,9 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     BR_GLOBAL double* wsg = launder(ws);
     constexpr int FR = NMAX;   // factor column stride (rows): [M: NMAX columns of NMAX rows | D^-1: 64]
     const LUWs F{wsg, wsg + NMAX * FR};
+    const __amdgpu_buffer_rsrc_t rs = lu_rsrc(wsg, NMAX * FR);   // the factor columns M
     lane = launder_v(lane);
     const int prow = launder_v(perm_io);      // original row held by this lane (lanes >= n: lane)
-    const int lc = min(lane, FR - 1);
     const bool act = lane < n;
     int pstep = act ? -1 : 1024;
     double dinv = 0.0;
@@ -1138,7 +1151,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (j < n && act) ? ldj(J + j * WAVE + prow) : 0.0;
             a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
         }
-        lu_rl_steps<P, FR>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, F);
+        lu_rl_steps<P, FR>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, rs);
     }
     BR_SUB_ADD(0, lt0);
     BR_SUB_T(lt1);
@@ -1150,30 +1163,41 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
             const double jv = (col < n && act) ? ldj(J + col * WAVE + prow) : 0.0;
             b[j] = ((col == prow) ? 1.0 : 0.0) - gamma * jv;
         }
-        // multipliers of panel 1 re-read from M, one chunk of CH steps ahead
-        double cur[CH], nxt[CH];
+        // multipliers of panel 1 re-read from M, one chunk of CH steps ahead (lanes >= FR read 0
+        // through the buffer range check)
+        const unsigned lo8 = (lane < FR) ? (unsigned)lane * 8u : LU_OOB;
+        auto ldm = [&](double (&v)[CH], int c0) {
 #pragma unroll
-        for (int i = 0; i < CH; ++i) cur[i] = (lane < FR) ? F.M[i * FR + lc] : 0.0;
-#pragma unroll 1
-        for (int kb = 0; kb < P; kb += CH) {
-            if (kb + CH < P) {
-#pragma unroll
-                for (int i = 0; i < CH; ++i) nxt[i] = (lane < FR) ? F.M[(kb + CH + i) * FR + lc] : 0.0;
-            }
+            for (int i = 0; i < CH; ++i)
+                v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo8 + i * (FR * 8), c0 * (FR * 8), 0));
+        };
+        auto ll_chunk = [&](const double (&cur)[CH], int kb) {
 #pragma unroll
             for (int i = 0; i < CH; ++i) {
                 const int k = kb + i;
                 const unsigned long long m = __ballot(pstep == k);
                 const int p = (int)__builtin_ctzll(m);
                 const double l = ((unsigned)pstep > (unsigned)k) ? cur[i] : 0.0;   // not pivoted by step k
+                // padding columns P + j >= n skipped; the bound is made opaque per step so each test
+                // stays a scalar compare and branch (hoisted, the tests became lane masks with two
+                // VALU ops per column and step to carry them)
+                int nl = n - P;
+                asm volatile("" : "+s"(nl));
 #pragma unroll
-                for (int j = 0; j < W2; ++j)   // (padding columns P + j >= n skipped: uniform branch)
-                    if (!BR_LL_SKIP || j + 8 < W2 || P + j < n) b[j] = fma(-bcast_lu(b[j], p), l, b[j]);
+                for (int j = 0; j < W2; ++j)
+                    if (j + 8 < W2 || j < nl) b[j] = fma(-bcast_lu(b[j], p), l, b[j]);
             }
+        };
+        double cur[CH], nxt[CH];
+        ldm(cur, 0);
+#pragma unroll 1
+        for (int kb = 0; kb < P; kb += CH) {
+            if (kb + CH < P) ldm(nxt, kb + CH);
+            ll_chunk(cur, kb);
 #pragma unroll
             for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
         }
-        lu_rl_steps<W2, FR>(b, P, n, n, lane, prow, pstep, dinv, fail, F);
+        lu_rl_steps<W2, FR>(b, P, n, n, lane, prow, pstep, dinv, fail, rs);
     }
     BR_SUB_ADD(1, lt1);
     BR_SUB_T(lt2);
