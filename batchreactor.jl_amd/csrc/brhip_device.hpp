@@ -202,19 +202,33 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 
 // quad_perm[1,0,3,2]=0xB1, quad_perm[2,3,0,1]=0x4E, row_half_mirror=0x141, row_mirror=0x140:
 // each step pairs lane i with a partner that pairs back with i, so both compute the same value.
+// Across the four row results: row_bcast:15 adds row 0 into row 1 and row 2 into row 3,
+// row_bcast:31 then row 1's total into row 3, and lane 63 is read: (r3 + r2) + (r1 + r0), equal
+// to (r0 + r1) + (r2 + r3) since each add is commutative (bit-identical to four readlanes).
+template <int CTRL, int RM>
+__device__ __forceinline__ double dppd_rows(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, RM, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, RM, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 __device__ __forceinline__ double wave_sum(double v) {
     v += dppd<0xB1>(v);
     v += dppd<0x4E>(v);
     v += dppd<0x141>(v);
     v += dppd<0x140>(v);
-    return (bcast(v, 0) + bcast(v, 16)) + (bcast(v, 32) + bcast(v, 48));
+    v = v + dppd_rows<0x142, 0xA>(v);   // (rows 0, 2 add 0: unused)
+    v = v + dppd_rows<0x143, 0xC>(v);
+    return bcast(v, 63);
 }
 __device__ __forceinline__ double wave_max(double v) {
     v = fmax(v, dppd<0xB1>(v));
     v = fmax(v, dppd<0x4E>(v));
     v = fmax(v, dppd<0x141>(v));
     v = fmax(v, dppd<0x140>(v));
-    return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
+    v = fmax(v, dppd_rows<0x142, 0xA>(v));
+    v = fmax(v, dppd_rows<0x143, 0xC>(v));
+    return bcast(v, 63);
 }
 
 // opaque copy of a uniform pointer: addresses derived from it cannot be hoisted out of the
@@ -231,6 +245,12 @@ __device__ __forceinline__ BR_GLOBAL T* launder(T* p) {
 // the identity-matrix entries of I - gamma*J out of the main loop)
 __device__ __forceinline__ int launder_v(int v) {
     asm volatile("" : "+v"(v));
+    return v;
+}
+// opaque copy of a uniform int (SGPR): comparisons against it are made where they are used
+// instead of being hoisted out of the integrator loop as lane masks (which then spill)
+__device__ __forceinline__ int launder_s(int v) {
+    asm volatile("" : "+s"(v));
     return v;
 }
 
@@ -1027,17 +1047,6 @@ __device__ __forceinline__ int pivot_lane(double a, unsigned cm, int prow) {
 // (A packed-triangle layout -- each sweep reading one triangle front to back, 25.5 KB instead of
 // ~29 KB per GRI solve from the fabric -- measured 2.7 % slower in round 3: its column segments
 // start at arbitrary 8-B offsets, so every load instruction spans one more 128-B line.)
-// saved-J loads of the LU (each line read once per factorization): optionally non-temporal
-#ifndef BR_LU_NT
-#define BR_LU_NT 0
-#endif
-__device__ __forceinline__ double ldj(const BR_GLOBAL double* p) {
-#if BR_LU_NT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
 struct LUWs {
     BR_GLOBAL double* M;
     BR_GLOBAL double* D;
@@ -1137,8 +1146,17 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     const LUWs F{wsg, wsg + NMAX * FR};
     const __amdgpu_buffer_rsrc_t rs = lu_rsrc(wsg, NMAX * FR);   // the factor columns M
     lane = launder_v(lane);
+    n = launder_s(n);
+    // the saved J through a buffer of n columns: a column j >= n, and any lane that holds no row,
+    // is out of range and reads 0 (no exec masks or per-column conditions; the column goes in the
+    // per-lane offset, whose immediate part covers 8 columns)
+    const __amdgpu_buffer_rsrc_t rj = __builtin_amdgcn_make_buffer_rsrc((void*)J, (short)0, n * (WAVE * 8), 0x00020000);
     const int prow = launder_v(perm_io);      // original row held by this lane (lanes >= n: lane)
     const bool act = lane < n;
+    const unsigned jo8 = act ? (unsigned)prow * 8u : LU_OOB;
+    auto ldj = [&](int col) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rj, jo8 + col * (WAVE * 8), 0, 0));
+    };
     int pstep = act ? -1 : 1024;
     double dinv = 0.0;
     int fail = 0;
@@ -1148,7 +1166,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
         double a[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            const double jv = (j < n && act) ? ldj(J + j * WAVE + prow) : 0.0;
+            const double jv = ldj(j);
             a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
         }
         lu_rl_steps<P, FR>(a, 0, n1, n1, lane, prow, pstep, dinv, fail, rs);
@@ -1160,7 +1178,7 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
 #pragma unroll
         for (int j = 0; j < W2; ++j) {
             const int col = P + j;
-            const double jv = (col < n && act) ? ldj(J + col * WAVE + prow) : 0.0;
+            const double jv = ldj(col);
             b[j] = ((col == prow) ? 1.0 : 0.0) - gamma * jv;
         }
         // multipliers of panel 1 re-read from M, one chunk of CH steps ahead (lanes >= FR read 0
