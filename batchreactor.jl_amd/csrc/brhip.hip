@@ -179,8 +179,11 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
     return w;
 }
 
-// uniform loads from the LDS controller
-__device__ __forceinline__ double ud(const LDbl& x) { return uni((double)x); }
+// loads from the LDS controller: ints through v_readfirstlane (SGPRs: scalar branches and loop
+// bounds); doubles stay in VGPRs (every lane reads the same value; fp64 arithmetic runs on the VALU
+// either way, and the two readfirstlanes per value were VALU instructions of their own: GRI +0.7 %,
+// surface-only +2.7 %, round 3)
+__device__ __forceinline__ double ud(const LDbl& x) { return (double)x; }
 __device__ __forceinline__ int ui(const __attribute__((address_space(3))) int& x) { return uni((int)x); }
 
 #ifndef BR_CTL_INLINE

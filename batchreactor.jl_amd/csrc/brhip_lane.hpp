@@ -105,7 +105,10 @@ struct ZH {
     }
 };
 
-#if BR_PHASE_CLOCKS
+#if BR_ASM_MARKS   // analysis builds: phase markers in the ISA listing
+#define LCLK(v) asm volatile("; BR_PHASE_BEGIN " #v)
+#define LACC(acc, v) asm volatile("; BR_PHASE_END " #acc)
+#elif BR_PHASE_CLOCKS
 #define LCLK(v) const unsigned long long v = clock64()
 #define LACC(acc, v) acc += clock64() - v
 #else
