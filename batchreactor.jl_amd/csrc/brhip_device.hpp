@@ -284,7 +284,9 @@ __device__ __forceinline__ void lds_add(double* p, double v) {
 }
 // acc[k] += nu_k * v over a reaction's net-stoichiometry scatter list (3 packed words)
 __device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, double v) {
-    const int cnt = (w1 >> 16) & 255;
+    // the count extracted once (opaque copy): otherwise each slot test became a v_mov of the slot
+    // number plus a byte-select compare
+    const int cnt = launder_v((int)((w1 >> 16) & 255));
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
         if (e < cnt) {
@@ -299,7 +301,7 @@ __device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, u
 // it in a register and reduces over the wave: in a Jacobian column pass nearly every entry of
 // column j touches species j, which made acc[j] the hot address of every atomic slot)
 __device__ __forceinline__ double scatter_noself(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, double v, int self) {
-    const int cnt = (w1 >> 16) & 255;
+    const int cnt = launder_v((int)((w1 >> 16) & 255));
     double sv = 0.0;
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
@@ -1418,12 +1420,13 @@ __device__ __forceinline__ int pivot_row2(double v0, bool c0, double v1, bool c1
 
 template <int W>
 __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, int cend, int lane, int (&pstep)[2],
-                                             double (&dinv)[2], int& fail, const LUWs& F, const int (&prow)[2]) {
+                                             double (&dinv)[2], int& fail, __amdgpu_buffer_rsrc_t rs, const int (&prow)[2]) {
     constexpr int CH = 8;
     static_assert(W % CH == 0, "W must be a multiple of 8");
     // the second slot's lanes 16..63 (positions 80..127, never rows) all address row 79: every
-    // value they hold or write there is 0 (padding rows), so no memory op needs an exec mask
-    const int o1 = min(64 + lane, CR2 - 1);
+    // value they hold or write there is 0 (padding rows), so no memory op needs an exec mask;
+    // factor stores as raw buffer ops (column base in soffset)
+    const unsigned fo8[2] = {(unsigned)lane * 8u, (unsigned)min(64 + lane, CR2 - 1) * 8u};
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
         const int pr = pivot_row2(fabs(a[0][0]), pstep[0] < 0, fabs(a[1][0]), pstep[1] < 0, prow);
@@ -1437,7 +1440,8 @@ __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, 
             const bool isp = (ps == s) && (lane == p);
             const bool rem = (pstep[s] < 0) && !isp;
             l[s] = rem ? a[s][0] * rinv : 0.0;
-            F.M[k * CR2 + (s ? o1 : lane)] = rem ? l[s] : ((pstep[s] >= 0) ? a[s][0] * dinv[s] : 0.0);
+            const double fv = rem ? l[s] : ((pstep[s] >= 0) ? a[s][0] * dinv[s] : 0.0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fv), rs, fo8[s], k * (CR2 * 8), 0);
             if (isp) { pstep[s] = k; dinv[s] = rinv; }
         }
         const int live = cend - k;
@@ -1470,31 +1474,36 @@ __device__ __forceinline__ void lu_rl_steps2(double (&a)[2][W], int k0, int k1, 
 // steps 0..C0-1 (multipliers from M in position order, masked to positions not yet pivoted at
 // that step), right-looking factorization of its own columns; then the next panel
 template <int NMAX, int C0>
-__device__ __forceinline__ void lu2_panels(const BR_GLOBAL double* J, double gamma, int n, int lane, int (&pstep)[2],
-                                           double (&dinv)[2], int& fail, const LUWs& F, const int (&prow)[2]) {
+__device__ __forceinline__ void lu2_panels(__amdgpu_buffer_rsrc_t rj, double gamma, int n, int lane, int (&pstep)[2],
+                                           double (&dinv)[2], int& fail, __amdgpu_buffer_rsrc_t rs, const int (&prow)[2]) {
     if constexpr (C0 < NMAX) {
         constexpr int W = (NMAX - C0) < 16 ? (NMAX - C0) : 16;
         if (C0 < n) {
-            const int o1 = min(64 + lane, CR2 - 1);   // (see lu_rl_steps2)
+            const unsigned fo8[2] = {(unsigned)lane * 8u, (unsigned)min(64 + lane, CR2 - 1) * 8u};   // (see lu_rl_steps2)
+            auto ldf = [&](int s, int col) {
+                return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, fo8[s], col * (CR2 * 8), 0));
+            };
             double a[2][W];
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int row = prow[s];
+                // J through a buffer of n columns: rows >= n and columns >= n are out of range (0)
+                const unsigned jo8 = (row < n) ? (unsigned)row * 8u : LU_OOB;
 #pragma unroll
                 for (int j = 0; j < W; ++j) {
                     const int col = C0 + j;
-                    const double jv = (col < n && row < n) ? J[col * CR2 + row] : 0.0;
+                    const double jv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rj, jo8 + col * (CR2 * 8), 0, 0));
                     a[s][j] = ((col == row) ? 1.0 : 0.0) - gamma * jv;
                 }
             }
             if (C0 > 0) {
-                double n0 = F.M[lane], n1 = F.M[o1];
+                double n0 = ldf(0, 0), n1 = ldf(1, 0);
 #pragma unroll 1
                 for (int k = 0; k < C0; ++k) {
                     const double m0 = n0, m1 = n1;
                     const int kn = (k + 1 < C0) ? k + 1 : k;
-                    n0 = F.M[kn * CR2 + lane];
-                    n1 = F.M[kn * CR2 + o1];
+                    n0 = ldf(0, kn);
+                    n1 = ldf(1, kn);
                     const unsigned long long b0 = __ballot(pstep[0] == k), b1 = __ballot(pstep[1] == k);
                     const int p = b0 ? (int)__builtin_ctzll(b0) : (int)__builtin_ctzll(b1);
                     const double l0 = ((unsigned)pstep[0] > (unsigned)k) ? m0 : 0.0;
@@ -1513,9 +1522,9 @@ __device__ __forceinline__ void lu2_panels(const BR_GLOBAL double* J, double gam
                 }
             }
             const int kend = (C0 + W < n) ? C0 + W : n;
-            lu_rl_steps2<W>(a, C0, kend, kend, lane, pstep, dinv, fail, F, prow);
+            lu_rl_steps2<W>(a, C0, kend, kend, lane, pstep, dinv, fail, rs, prow);
         }
-        lu2_panels<NMAX, C0 + 16>(J, gamma, n, lane, pstep, dinv, fail, F, prow);
+        lu2_panels<NMAX, C0 + 16>(rj, gamma, n, lane, pstep, dinv, fail, rs, prow);
     }
 }
 
@@ -1529,7 +1538,10 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
     const BR_GLOBAL double* J = launder(J_);
     BR_GLOBAL double* wsg = launder(ws);
     const LUWs F{wsg, wsg + NMAX * CR2};
+    const __amdgpu_buffer_rsrc_t rs = lu_rsrc(wsg, NMAX * CR2);   // the factor columns M
     lane = launder_v(lane);
+    n = launder_s(n);
+    const __amdgpu_buffer_rsrc_t rj = __builtin_amdgcn_make_buffer_rsrc((void*)J, (short)0, n * (CR2 * 8), 0x00020000);
     int pstep[2], prow[2];
     double dinv[2] = {0.0, 0.0};
     int fail = 0;
@@ -1539,7 +1551,7 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
         prow[s] = (pos < n) ? launder_v(perm_io[s]) : pos;
         pstep[s] = (pos < n) ? -1 : 1024;
     }
-    lu2_panels<NMAX, 0>(J, gamma, n, lane, pstep, dinv, fail, F, prow);
+    lu2_panels<NMAX, 0>(rj, gamma, n, lane, pstep, dinv, fail, rs, prow);
     const int o1 = min(64 + lane, CR2 - 1);   // (see lu_rl_steps2)
     if (__ballot((lane < n && pstep[0] != lane) || (lane + 64 < n && pstep[1] != lane + 64)) == 0) {
         // every pivot on its own position: M is in step order already; D^-1 in step order

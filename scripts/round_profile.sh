@@ -21,6 +21,8 @@ for c in $CFGS; do
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], round(d['value']), round(r['kernel_ms'],1), 'frac', round(r['frac'],4), 'traffic/reactor', (r['traffic'] or 0)/d['config']['reactors_rank0'])" gpurun_out/profiles/${TAG}_bench_$c.json $c
 done
 if [[ " $CFGS " == *" gri "* ]]; then
+  # SQ instruction mix / VALU-busy counters (two passes) -> profiles/${TAG}_pmc_sq_gri.json
+  bash scripts/pmc_sq.sh gri 20000 > gpurun_out/pmc_sq_gri.log 2>&1 && cp gpurun_out/sq_gri.json gpurun_out/profiles/${TAG}_pmc_sq_gri.json || { echo "pmc_sq failed"; tail -5 gpurun_out/pmc_sq_gri.log; exit 1; }
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --no-phase --no-pcie > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; exit 1; }
   cp "$(ls gpurun_out/prof/*kernel_stats.csv | head -1)" gpurun_out/profiles/${TAG}_gri1e5_kernel_stats.csv
   grep "^{\"metric\"" gpurun_out/prof.log | tail -1 > gpurun_out/profiles/${TAG}_gri1e5_rocprof_bench_line.json
