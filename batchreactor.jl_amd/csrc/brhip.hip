@@ -1383,7 +1383,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     DevMech& M = m->dm;
     M.ng = ng; M.ns = ns; M.n = n; M.nrg = nrg; M.nrs = nrs; M.conv = d->conv;
     M.cpl = n > 64 ? 2 : 1;
-    const int SPW = 64 * M.cpl;                                   // species slots (Lay<CPL>::SPW)
+    const int SPW = M.cpl == 2 ? Lay<2>::SPW : Lay<1>::SPW;       // species slots
     const int SP_ONE = M.cpl == 2 ? Lay<2>::ONE : Lay<1>::ONE;    // pad species: conc = 1
     const int IMG_RX_OFF = M.cpl == 2 ? Lay<2>::IMG_RX : Lay<1>::IMG_RX;
     M.p_std = d->p_std > 0 ? d->p_std : 1e5;

@@ -110,7 +110,9 @@ constexpr int RX_WORDS = 8, SX_WORDS = 12, SXE_DOUBLES = 8;
 // arrays and the table image are sized SPW = 64 * CPL.
 template <int CPL>
 struct Lay {
-    static constexpr int SPW = 64 * CPL;
+    // species slots: 64, or 80 for two components per lane (n <= 72; round 3: 128 before, the LDS
+    // saved per reactor lets 12 gas+surface reactors share a CU instead of 11)
+    static constexpr int SPW = CPL == 2 ? 80 : 64;
     // species block (doubles): conc[SPW], conc[ONE] = 1.0 (pad species of the packed records),
     // accw[SPW], accs[SPW], mc[64] third-body concentration per efficiency set
     static constexpr int CONC = 0, ONE = SPW, ACCW = SPW + 16, ACCS = 2 * SPW + 16, MC = 3 * SPW + 16;
@@ -1389,7 +1391,7 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
 // order (prow: position -> original row), so when every pivot lands on its own position the
 // factors are already in step order and the gather pass is skipped. The panels are 16 columns
 // wide (registers: 2 x 16 per lane); the inverse permutation, P b and D^-1 go through LDS scratch
-// (>= 256 doubles).
+// (>= 160 doubles).
 // ------------------------------------------------------------------------------------
 constexpr int CR2 = 80;
 
@@ -1567,25 +1569,30 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
     }
     // inverse permutation through LDS: position of step s (positions >= n map to themselves),
     // and the original row / D^-1 of every position
-    LDSi* isc = (LDSi*)scr;            // [128] step -> position
-    LDSi* rsc = (LDSi*)(scr + 64);     // [128] position -> original row
-    LDSd* dsc = scr + 128;             // [128] position -> D^-1
+    // (positions >= CR2 are padding and map to themselves, so the tables hold CR2 entries: 160
+    // doubles of the scratch)
+    LDSi* isc = (LDSi*)scr;            // [CR2] step -> position
+    LDSi* rsc = (LDSi*)(scr + 40);     // [CR2] position -> original row
+    LDSd* dsc = scr + 80;              // [CR2] position -> D^-1
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const int pos = lane + 64 * s;
-        isc[(pos < n) ? pstep[s] : pos] = pos;
-        rsc[pos] = prow[s];
-        dsc[pos] = dinv[s];
+        if (pos < CR2) {
+            isc[(pos < n) ? pstep[s] : pos] = pos;
+            rsc[pos] = prow[s];
+            dsc[pos] = dinv[s];
+        }
     }
     wave_sync();
     int q[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        q[s] = isc[lane + 64 * s];
-        perm_io[s] = rsc[q[s]];
+        const int pos = lane + 64 * s;
+        q[s] = (pos < CR2) ? isc[pos] : pos;
+        perm_io[s] = (q[s] < CR2) ? rsc[q[s]] : pos;
     }
     F.D[lane] = dsc[q[0]];
-    F.D[o1] = dsc[q[1]];
+    F.D[o1] = (q[1] < CR2) ? dsc[q[1]] : 0.0;
     wave_sync();
     // positions into step order, in place, chunks of CH columns double-buffered (columns >= n: zeros)
     double g[2][2][CH];
@@ -1721,11 +1728,12 @@ __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* s
                                           const int (&perm)[2], double (&b)[2]) {
     const BR_GLOBAL double* wsg = launder(ws);
     lane = launder_v(lane);
-    LDSd* dsc = scr + 128;
+    LDSd* dsc = scr + 64;   // [CR2] (scr[0..63]: the sweeps' copy row)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) dsc[lane + 64 * s] = (lane + 64 * s < n) ? b[s] : 0.0;
+    for (int s = 0; s < 2; ++s)
+        if (lane + 64 * s < CR2) dsc[lane + 64 * s] = (lane + 64 * s < n) ? b[s] : 0.0;
     wave_sync();
-    double r[2] = {dsc[perm[0]], dsc[perm[1]]};   // P b
+    double r[2] = {dsc[perm[0]], (perm[1] < CR2) ? dsc[perm[1]] : 0.0};   // P b
     wave_sync();
     static_assert(NMAX > 64 && NMAX <= 72, "lu_solve2: NMAX");
     // (all solve loads are buffer loads: drain first so the waitcnt pass can count them in order)
