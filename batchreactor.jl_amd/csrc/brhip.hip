@@ -2082,8 +2082,14 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
+    // twice, as in the integrator: the first factorization loads the rows in natural order (pivot
+    // search + gather path), the second in the first one's pivot order (every pivot on its own lane:
+    // the factors come out in step order, no gather); the solve uses the second one's factors
     int perm = lane;
-    const int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+    int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0, (LDSd*)prow);
