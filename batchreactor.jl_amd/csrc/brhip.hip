@@ -1394,8 +1394,13 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         return w;
     };
     // net-stoichiometry scatter list of a reaction: up to 6 (species, nu != 0) pairs packed in
-    // 3 words: w0 = species 0..3, w1 = species 4..5 | count << 16, w2 = 4-bit signed nu x 6
-    auto scatter_pack = [](const int* f, int nf, const int* pr, int np, uint32_t* w) -> bool {
+    // 4 words (brhip_device.hpp sl_off / sl_nu): w0..w2 = byte offsets species * 8 of slots 0..5,
+    // two 16-bit fields per word; w3 = 4-bit signed nu x 6 | count << 24
+    auto sl_put = [](uint32_t* w, int t, int sp, int nu) {
+        w[t >> 1] |= (uint32_t)(sp * 8) << (16 * (t & 1));
+        w[3] |= (uint32_t)(nu & 15) << (4 * t);
+    };
+    auto scatter_pack = [&sl_put](const int* f, int nf, const int* pr, int np, uint32_t* w) -> bool {
         int sp[12], nu[12], c = 0;
         auto add = [&](int k, int v) {
             for (int i = 0; i < c; ++i) if (sp[i] == k) { nu[i] += v; return; }
@@ -1404,16 +1409,14 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         for (int e = 0; e < nf; ++e) add(f[e], -1);
         for (int e = 0; e < np; ++e) add(pr[e], 1);
         int mm = 0;
-        w[0] = w[1] = w[2] = 0;
+        w[0] = w[1] = w[2] = w[3] = 0;
         for (int i = 0; i < c; ++i) {
             if (nu[i] == 0) continue;
-            if (mm >= 6 || nu[i] < -8 || nu[i] > 7) return false;
-            if (mm < 4) w[0] |= (uint32_t)(sp[i] & 255) << (8 * mm);
-            else w[1] |= (uint32_t)(sp[i] & 255) << (8 * (mm - 4));
-            w[2] |= (uint32_t)(nu[i] & 15) << (4 * mm);
+            if (mm >= 6 || nu[i] < -8 || nu[i] > 7 || sp[i] < 0 || sp[i] > 255) return false;
+            sl_put(w, mm, sp[i], nu[i]);
             ++mm;
         }
-        w[1] |= (uint32_t)mm << 16;
+        w[3] |= (uint32_t)mm << 24;
         return true;
     };
     // ---- gas reactions, evaluated in a permuted order (falloff, then +M, then elementary) so
@@ -1523,17 +1526,17 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
     //      H, O, OH, H2O ...). Per group of 64 reactions, each reaction's list is permuted so that its
     //      species land in the slots where they are least used so far (greedy, exhaustive over the
     //      <= 720 orders of one list). Only the order of the per-species sums changes.
-    auto spread_slots = [](std::vector<uint32_t>& recs, int words, int off, int nrec) {
+    auto spread_slots = [&sl_put](std::vector<uint32_t>& recs, int words, int off, int nrec) {
         for (int g0 = 0; g0 < nrec; g0 += WAVE) {
             static thread_local int cnt[6][256];
             memset(cnt, 0, sizeof(cnt));
             for (int i = g0; i < std::min(nrec, g0 + WAVE); ++i) {
                 uint32_t* w = &recs[(size_t)words * i + off];
-                const int m = (w[1] >> 16) & 255;
+                const int m = (int)(w[3] >> 24);
                 int sp[6], nu[6], ord[6], best[6];
                 for (int e = 0; e < m; ++e) {
-                    sp[e] = e < 4 ? (w[0] >> (8 * e)) & 255 : (w[1] >> (8 * (e - 4))) & 255;
-                    nu[e] = ((int)(w[2] << (28 - 4 * e))) >> 28;
+                    sp[e] = (int)(((w[e >> 1] >> (16 * (e & 1))) & 0xffffu) >> 3);
+                    nu[e] = ((int)(w[3] << (28 - 4 * e))) >> 28;
                     ord[e] = e;
                 }
                 long bc = -1;
@@ -1542,15 +1545,13 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
                     for (int t = 0; t < m; ++t) { const long v = cnt[t][sp[ord[t]]] + 1; c += v * v; }
                     if (bc < 0 || c < bc) { bc = c; std::copy(ord, ord + m, best); }
                 } while (std::next_permutation(ord, ord + m));
-                uint32_t w0 = 0, w1 = w[1] & ~0xFFFFu, w2 = w[2] & 0xFF000000u;
+                uint32_t nw[4] = {0, 0, 0, w[3] & 0xFF000000u};
                 for (int t = 0; t < m; ++t) {
                     const int e = best[t];
-                    if (t < 4) w0 |= (uint32_t)sp[e] << (8 * t);
-                    else w1 |= (uint32_t)sp[e] << (8 * (t - 4));
-                    w2 |= (uint32_t)(nu[e] & 15) << (4 * t);
+                    sl_put(nw, t, sp[e], nu[e]);
                     cnt[t][sp[e]]++;
                 }
-                w[0] = w0; w[1] = w1; w[2] = w2;
+                for (int q = 0; q < 4; ++q) w[q] = nw[q];
             }
         }
     };

@@ -284,17 +284,25 @@ __device__ __forceinline__ RView rview(char* spbase, const DevMech& /*M*/, BR_GL
 __device__ __forceinline__ void lds_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
-// acc[k] += nu_k * v over a reaction's net-stoichiometry scatter list (3 packed words)
-__device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, double v) {
+// Net-stoichiometry scatter list of a reaction (4 packed words): w0..w2 hold the byte offsets
+// (species * 8) of slots 0..5, two 16-bit fields per word, w3 the 4-bit signed nu of each slot |
+// count << 24. Byte offsets: a slot's address is one add of the field to the array base (a
+// select-word add) instead of a byte extract and a shift-add (round 3: the production loop's
+// scatter is ~1/3 of the RHS's VALU).
+__device__ __forceinline__ unsigned sl_off(uint32_t w, int hi) { return hi ? (w >> 16) : (w & 0xffffu); }
+__device__ __forceinline__ int sl_nu(uint32_t w3, int e) { return ((int)(w3 << (28 - 4 * e))) >> 28; }
+// acc[k] += nu_k * v over the list
+__device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, double v) {
     // the count extracted once (opaque copy): otherwise each slot test became a v_mov of the slot
     // number plus a byte-select compare
-    const int cnt = launder_v((int)((w1 >> 16) & 255));
+    const int cnt = launder_v((int)(w3 >> 24));
+    const uint32_t ws[3] = {w0, w1, w2};
+    char* const base = reinterpret_cast<char*>(acc);
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
         if (e < cnt) {
-            const int k = e < 4 ? sp8(w0, e) : sp8(w1, e - 4);
-            const int nu = ((int)(w2 << (28 - 4 * e))) >> 28;   // sign-extended nibble
-            lds_add(&acc[k], (double)nu * v);                    // exact for small integer nu
+            double* p = reinterpret_cast<double*>(base + sl_off(ws[e >> 1], e & 1));
+            lds_add(p, (double)sl_nu(w3, e) * v);                // exact for small integer nu
         }
     }
 }
@@ -302,17 +310,20 @@ __device__ __forceinline__ void scatter(double* acc, uint32_t w0, uint32_t w1, u
 // scatter() except for species `self`: its nu * v is returned instead of added (the caller sums
 // it in a register and reduces over the wave: in a Jacobian column pass nearly every entry of
 // column j touches species j, which made acc[j] the hot address of every atomic slot)
-__device__ __forceinline__ double scatter_noself(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, double v, int self) {
-    const int cnt = launder_v((int)((w1 >> 16) & 255));
+__device__ __forceinline__ double scatter_noself(double* acc, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, double v,
+                                                 int self) {
+    const int cnt = launder_v((int)(w3 >> 24));
+    const uint32_t ws[3] = {w0, w1, w2};
+    const unsigned self8 = (unsigned)self * 8u;
+    char* const base = reinterpret_cast<char*>(acc);
     double sv = 0.0;
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
         if (e < cnt) {
-            const int k = e < 4 ? sp8(w0, e) : sp8(w1, e - 4);
-            const int nu = ((int)(w2 << (28 - 4 * e))) >> 28;
-            const double t = (double)nu * v;
-            if (k == self) sv += t;
-            else lds_add(&acc[k], t);
+            const unsigned off = sl_off(ws[e >> 1], e & 1);
+            const double t = (double)sl_nu(w3, e) * v;
+            if (off == self8) sv += t;
+            else lds_add(reinterpret_cast<double*>(base + off), t);
         }
     }
     return sv;
@@ -519,8 +530,8 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
         const uint4 rb1 = *reinterpret_cast<const uint4*>(rr1.b);
         const double D0 = rate(r, ra0, k0);
         const double D1 = rate(q1, ra1, k1);
-        scatter(accw, rb0.x, rb0.y, rb0.z, D0);
-        if (has1) scatter(accw, rb1.x, rb1.y, rb1.z, D1);
+        scatter(accw, rb0.x, rb0.y, rb0.z, rb0.w, D0);
+        if (has1) scatter(accw, rb1.x, rb1.y, rb1.z, rb1.w, D1);
     }
 #pragma unroll 1
     for (int r = lane; r < MF(nrs); r += WAVE) {
@@ -538,7 +549,7 @@ __device__ __forceinline__ void production(const DevMech& M, const Tab& tb_, con
         // branch-free product over up to 6 reactants (pad slots = conc[L::ONE] = 1)
         const double P = ((conc[sp8(rec[0], 0)] * conc[sp8(rec[0], 1)]) * (conc[sp8(rec[0], 2)] * conc[sp8(rec[0], 3)])) *
                          (conc[sp8(rec[1], 0)] * conc[sp8(rec[1], 1)]);
-        scatter(accs, rec[6], rec[7], rec[8], k * P);
+        scatter(accs, rec[6], rec[7], rec[8], rec[9], k * P);
     }
 }
 
@@ -664,7 +675,7 @@ __device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int
         if (st < nset) {
             if (lane < n) accw[lane] = 0.0;
             wave_sync();
-            if (lane < ntb && (int)tbset == st) scatter(accw, recl[4], recl[5], recl[6], dcm);
+            if (lane < ntb && (int)tbset == st) scatter(accw, recl[4], recl[5], recl[6], recl[7], dcm);
             wave_sync();
             w[st] = (lane < n) ? accw[lane] : 0.0;
             wave_sync();
@@ -727,7 +738,7 @@ __device__ __forceinline__ void jacobian_fast(const Tab& tb, const RView& R, int
                 for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= conc[sp8(rec[1], e2)];
                 d -= pr;
             }
-            const double sv = scatter_noself(acc, rec[4], rec[5], rec[6], d, j);
+            const double sv = scatter_noself(acc, rec[4], rec[5], rec[6], rec[7], d, j);
             if (i >= c2) sf2 += sv;
             else if (i >= c1) sf1 += sv;
             else sf0 += sv;
@@ -876,7 +887,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                     d -= pre * pr;
                 }
                 if (tbk && j < MF(ng)) d += ld_l2(jscr + 2 * r + 1) * MF(tb_eff)[gi_tbidx(info) * n + j];
-                scatter(acc, rec[4], rec[5], rec[6], d);
+                scatter(acc, rec[4], rec[5], rec[6], rec[7], d);
             }
             wave_sync();
             BR_SUB_ADD(4, jt2);
@@ -930,7 +941,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                     d -= pre * pr;
                 }
                 if (tbk && j < MF(ng)) d += ld_l2(jscr + 2 * r + 1) * MF(tb_eff)[gi_tbidx(info) * MF(n) + j];
-                scatter(accw, rec[4], rec[5], rec[6], d);
+                scatter(accw, rec[4], rec[5], rec[6], rec[7], d);
             } else {
                 const int r = rr - MF(nrg);
                 const uint32_t* rec = tb.sx + SX_WORDS * r;
@@ -967,7 +978,7 @@ __device__ __forceinline__ void jacobian(const DevMech& M, const Tab& tb_, const
                     for (int jj = 0; jj < 4; ++jj) if (jj < nc && sp8(rec[5], jj) == j)
                         d += q * (-tb.sxe[SXE_DOUBLES * r + jj] / RT);
                 }
-                scatter(accs, rec[6], rec[7], rec[8], d);
+                scatter(accs, rec[6], rec[7], rec[8], rec[9], d);
             }
         }
         wave_sync();

@@ -948,7 +948,7 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
     }
     for (int r = 0; r < nrg; ++r) {
         const auto rec = rx_rec(rx, r);
-        const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], s0 = rec[4], s1 = rec[5], s2 = rec[6];
+        const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], sw[4] = {rec[4], rec[5], rec[6], rec[7]};
         const double kf = kq[0][0], kr = kq[0][1];
 #pragma unroll
         for (int d = 0; d < PF - 1; ++d) { kq[d][0] = kq[d + 1][0]; kq[d][1] = kq[d + 1][1]; }
@@ -982,12 +982,12 @@ __device__ __forceinline__ void lane_rhs(const LaneLay& LL, double* Lp, const GR
                 if (xm) D *= Mc * 1e-6;                         // [M] in mol/cm3
             }
         }
-        const int cnt = (s1 >> 16) & 255;
+        const int cnt = (int)(sw[3] >> 24);
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
             if (e < cnt) {
-                const int k = e < 4 ? (int)((s0 >> (8 * e)) & 255) : (int)((s1 >> (8 * (e - 4))) & 255);
-                const int nu = ((int)(s2 << (28 - 4 * e))) >> 28;
+                const int k = (int)(sl_off(sw[e >> 1], e & 1) >> 3);
+                const int nu = sl_nu(sw[3], e);
                 lds_add(&Lp[(LL.acc + k) * 64], (double)nu * D);
             }
         }
@@ -1015,7 +1015,7 @@ __device__ __forceinline__ void lane_jac(const LaneLay& LL, const double* Lp, co
         for (int i = 0; i < NM; ++i) G.st(j * NM + i, 0.0);
     for (int r = 0; r < nrg; ++r) {
         const auto rec = rx_rec(rx, r);
-        const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], s0 = rec[4], s1 = rec[5], s2 = rec[6];
+        const uint32_t w0 = rec[0], w1 = rec[1], info = rec[2], sw[4] = {rec[4], rec[5], rec[6], rec[7]};
         const double kf = G.ld(LL.g_rxd + 2 * r), kr = G.ld(LL.g_rxd + 2 * r + 1);
         double cf[4], cb[4];
 #pragma unroll
@@ -1066,10 +1066,11 @@ __device__ __forceinline__ void lane_jac(const LaneLay& LL, const double* Lp, co
                 dq[j] += (j == kbs) ? pb : 0.0;
             }
         }
-        const int cnt = (s1 >> 16) & 255;
+        const int cnt = (int)(sw[3] >> 24);
         for (int e = 0; e < cnt; ++e) {                                // rows of the touched species
-            const int k = e < 4 ? (int)((s0 >> (8 * e)) & 255) : (int)((s1 >> (8 * (e - 4))) & 255);
-            const int nu = ((int)(s2 << (28 - 4 * e))) >> 28;
+            const uint32_t we = (e >> 1) == 0 ? sw[0] : ((e >> 1) == 1 ? sw[1] : sw[2]);   // (uniform selects)
+            const int k = (int)(sl_off(we, e & 1) >> 3);
+            const int nu = sl_nu(sw[3], e);
             const double sk = (double)nu * mw[k];
 #pragma unroll
             for (int j = 0; j < NM; ++j)
