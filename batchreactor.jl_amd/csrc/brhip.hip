@@ -24,6 +24,18 @@
 #define BR_PHASE_CLOCKS 0   // per-phase shader-clock counters in br_stats (diagnostic build: libbrhip_diag.so)
 #endif
 #include "brhip_device.hpp"
+// Diagnostic-only instruction-count experiments (scripts/micro/exp_hooks.hpp: a phase run twice,
+// extra VALU or memory work per Newton iteration) attach at these points of k_integrate; the
+// product build leaves them empty.
+#ifdef BR_EXPERIMENT_HOOKS
+#include BR_EXPERIMENT_HOOKS
+#endif
+#ifndef BR_X_AFTER_RHS
+#define BR_X_AFTER_RHS()
+#define BR_X_AFTER_JAC()
+#define BR_X_AFTER_SOLVE()
+#define BR_X_AFTER_ITER()
+#endif
 
 using namespace brhip;
 
@@ -48,7 +60,7 @@ struct KOpts {
     int nout;                 // dense output: tout[nout] (device), yout[N][nout][n] (device)
     const double* tout;
     double* yout;
-    int dq_jac;               // k_lane: CVODE's DQ Jacobian (br_opts.dq_jacobian) instead of the analytic one
+    int dq_jac;               // CVODE's DQ Jacobian (br_opts.dq_jacobian) instead of the analytic one (both engines)
     int defer_steps;          // k_lane: hand a reactor still running after this many steps to the
                               // wavefront engine (restart from u0); >= max_steps disables
     const int* rid_list;      // k_integrate: integrate reactors rid_list[0 .. min(*rid_count, N)) only
@@ -81,6 +93,8 @@ struct Ctl {
     int callSetup, jbad, jcur_nls, hnewOK, newj;
     // ignition marker (max dX_ign/dt over accepted steps) and dense-output cursor
     double ign_x, ign_t, ign_rate, t_ign, ign_dt;
+    double dq_mininc;         // CVODE's DQ Jacobian: minInc of the Jacobian being built
+    int nfe_dq;               // RHS evaluations of the DQ Jacobian (CVODE's nfeDQ)
     int iout;
     // per-launch constants (here rather than in registers: they are read once per step)
     double a_rtol, a_atol, a_hmax_inv, a_ufac;
@@ -932,6 +946,57 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     return A_RHS;
 }
 
+// ---- CVODE's dense difference-quotient Jacobian (cvLsDenseDQJac; CVODE_BDF()'s default, no `jac`
+// is passed to ODEProblem at src/BatchReactor.jl:140,:204): at the setup point (y = z0, fy = F(y)),
+// column j = (F(y + inc_j e_j) - fy) / inc_j with inc_j = max(sqrt(uround) |y_j|, minInc / ewt_j),
+// minInc = 1000 |h| uround n ||fy||_WRMS (1 if that norm is 0). One RHS per column, run through the
+// kernel's single RHS call site (k_integrate: the column index `dqj` routes the result here).
+constexpr double DQ_SRUR = 1.4901161193847656e-08;   // sqrt(UROUND) = 2^-26
+constexpr double DQ_MIN_INC_MULT = 1000.0;
+template <int CPL>
+__device__ __forceinline__ void dq_begin(LCtl* C, VT<CPL>& V, int lane, const double (&f)[CPL]) {
+    const int n = ui(C->a_n);
+    double ewt[CPL];
+#pragma unroll
+    FOR_S {
+        ewt[s] = V.at(V_EWT, s);
+        V.at(V_TEMP, s) = f[s];                      // fy, kept for the n columns
+    }
+    const double fnorm = wrms_l<CPL>(f, ewt, lane, n);
+    C->dq_mininc = (fnorm != 0.0) ? (DQ_MIN_INC_MULT * fabs(ud(C->h)) * UROUND * n * fnorm) : 1.0;
+}
+// increment of this lane's components (the one for component j is used by column j)
+template <int CPL>
+__device__ __forceinline__ void dq_incs(LCtl* C, VT<CPL>& V, int lane, double (&inc)[CPL]) {
+    const double mininc = ud(C->dq_mininc);
+#pragma unroll
+    FOR_S inc[s] = fmax(DQ_SRUR * fabs(V.at(V_Z0, s)), mininc / V.at(V_EWT, s));
+}
+// column j of the saved J from F(y + inc_j e_j) = f (rows as jacobian(): JW per column)
+template <int CPL>
+__device__ __forceinline__ void dq_column(LCtl* C, VT<CPL>& V, int lane, int j, const double (&f)[CPL], double* Jsave) {
+    constexpr int JW = CPL == 2 ? 80 : 64;
+    double inc[CPL];
+    dq_incs<CPL>(C, V, lane, inc);
+    const double ij = (j < 64) ? bcast(inc[0], j) : bcast(inc[CPL - 1], j - 64);
+    const double ii = 1.0 / ij;
+    BR_GLOBAL double* col = launder(Jsave) + (size_t)j * JW;
+#pragma unroll
+    FOR_S {
+        const double v = ii * f[s] - ii * V.at(V_TEMP, s);
+        if (s == 0) col[lane] = v;
+        else if (lane < 16) col[64 + lane] = v;
+    }
+    C->nfe_dq = ui(C->nfe_dq) + 1;
+}
+// the Newton right-hand side at the setup point again (cvNlsResidual with f = fy, as ctl_post_rhs)
+template <int CPL>
+__device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL>& V, int lane, double (&b)[CPL]) {
+    const double rl1 = ud(C->rl1), gamma = ud(C->gamma);
+#pragma unroll
+    FOR_S b[s] = -((rl1 * V.at(1, s) + V.at(V_ACOR, s)) - gamma * V.at(V_TEMP, s));
+}
+
 #include "brhip_lane.hpp"   // one reactor per lane (small gas mechanisms)
 
 // ------------------------------------------------------------------------------------
@@ -939,6 +1004,9 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
 // ------------------------------------------------------------------------------------
 #ifndef BR_WPE
 #define BR_WPE 2
+#endif
+#ifndef BR_LU_MFMA
+#define BR_LU_MFMA 1   // 32 < NMAX <= 64: blocked LU with MFMA trailing updates (lu_factor_mf)
 #endif
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
@@ -1042,12 +1110,14 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     C->count1 = 0; C->phase = PH_F0; C->callSetup = 0; C->jbad = 0; C->jcur_nls = 0; C->hnewOK = 0; C->newj = 0;
     C->p_last = 0.0;
     C->iout = 0; C->ign_t = t0; C->ign_rate = -INFINITY; C->t_ign = NAN; C->ign_x = 0.0; C->ign_dt = NAN;
+    C->dq_mininc = 1.0; C->nfe_dq = 0;
     if (o.ign >= 0) C->ign_x = uni(mole_frac_of<CPL>(u0, lane, o.ign));
     // counters and ignition marker of the lane pass (deferred reactors) to continue from
     double st_in[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (o.rid_t0 && stats) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) st_in[k] = uni(stats[(size_t)rid * BR_NSTAT + k]);
+        st_in[7] = uni(stats[(size_t)rid * BR_NSTAT + 19]);   // nfe_dq
         // the step limit is on the whole run (SciML maxiters): the lane pass's steps count against it
         C->a_max_steps = max(o.max_steps - (int)st_in[0], 0);
         if (o.ign >= 0) {
@@ -1085,40 +1155,66 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     FOR_S perm[s] = CS;
     LDSd* scr = (LDSd*)(S.sp + Lay<CPL>::ACCW);   // solve / LU scratch: the production sums are idle then
     double* p_last = reinterpret_cast<double*>(W.rbase);   // Ctl::p_last is the first field
+    int dqj = -1;   // >= 0: building DQ Jacobian column dqj (this RHS is at y + inc_dqj e_dqj)
     for (;;) {
         double y[CPL], f[CPL];
 #pragma unroll
         FOR_S y[s] = V.at(V_Y, s);
+        if (dqj >= 0) {
+            double inc[CPL];
+            dq_incs<CPL>(C, V, lane, inc);
+#pragma unroll
+            FOR_S if (CS == dqj) y[s] += inc[s];
+        }
         {
             BR_CLK(c0);
             rhs<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, p_last, f);
-#if defined(BR_EXP_DUP) && BR_EXP_DUP == 1   // experiment: the RHS twice (phase instruction counts)
-            asm volatile("" ::: "memory");
-            rhs<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, p_last, f);
-#endif
+            BR_X_AFTER_RHS();
             BR_ACC(cyc_rhs, c0);
         }
         double b[CPL];
-        BR_CLK(c2);
-        BR_SUB_T(pr0);
-        int act_code = ctl_post_rhs<CPL>(C, V, lane, f, b);
-        BR_SUB_ADD(3, pr0);
-        BR_ACC(cyc_ctl, c2);
-        if (act_code == A_RHS) continue;
-        if (act_code == A_DONE) break;
+        int act_code;
+        bool jac_ready = false;
+        if (dqj >= 0) {   // a DQ column (its RHS counts in nfe_dq, not nfe)
+            BR_CLK(c0);
+            dq_column<CPL>(C, V, lane, dqj, f, Jsave);
+            BR_ACC(cyc_jac, c0);
+            if (++dqj < n) continue;
+            dqj = -1;
+            dq_newton_rhs<CPL>(C, V, lane, b);
+            act_code = A_SETUP;
+            jac_ready = true;
+        } else {
+            BR_CLK(c2);
+            BR_SUB_T(pr0);
+            act_code = ctl_post_rhs<CPL>(C, V, lane, f, b);
+            BR_SUB_ADD(3, pr0);
+            BR_ACC(cyc_ctl, c2);
+            if (act_code == A_RHS) continue;
+            if (act_code == A_DONE) break;
+            if (act_code == A_SETUP && o.dq_jac && ui(C->newj)) {
+                dq_begin<CPL>(C, V, lane, f);
+                dqj = 0;
+                continue;
+            }
+        }
         int lu_fail = 0;
         if (act_code == A_SETUP) {
-            if (ui(C->newj)) {
+            if (!jac_ready && ui(C->newj)) {
                 BR_CLK(c0);
                 jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
-#if defined(BR_EXP_DUP) && BR_EXP_DUP == 3   // experiment: the Jacobian twice
-                asm volatile("" ::: "memory");
-                jacobian<CPL>(M, tb, S, T, Asv, Asv_th, y, lane, Jsave, jscr);
-#endif
+                BR_X_AFTER_JAC();
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
+            if constexpr (CPL == 1 && NMAX > 32 && BR_LU_MFMA) {
+                // blocked LU, trailing updates on the fp64 matrix pipe; its E' staging uses the
+                // species block (idle between the Jacobian and the next RHS), whose conc[ONE] = 1.0
+                // pad slot (set once per reactor by init_tconst) is put back afterwards
+                lu_fail = lu_factor_mf<NMAX>(Jsave, LUsave, (LDSd*)S.sp, ud(C->gamma), n, lane, perm[0]);
+                wave_sync();
+                if (lane == 0) S.sp[Lay<CPL>::ONE] = 1.0;
+            } else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
         }
@@ -1127,45 +1223,17 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
         FOR_S delta[s] = 0.0;
         if (!lu_fail) {
             BR_CLK(c0);
-            if constexpr (CPL == 1) delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
-#if defined(BR_EXP_DUP) && BR_EXP_DUP == 2   // experiment: the solve twice
             if constexpr (CPL == 1) {
-                asm volatile("" ::: "memory");
-                double d2 = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
-                asm volatile("" : "+v"(d2));
-                delta[0] = d2;
-            }
-#endif
-            else {
+                delta[0] = lu_solve<NMAX>(LUsave, n, lane, perm[0], b[0], scr);
+                BR_X_AFTER_SOLVE();
+            } else {
                 lu_solve2<NMAX>(LUsave, scr, n, lane, perm, b);
                 delta[0] = b[0];
                 delta[1] = b[1];
             }
             BR_ACC(cyc_sol, c0);
         }
-#ifdef BR_EXP_VALU   // experiment: BR_EXP_VALU independent dummy fp64 FMAs per Newton iteration
-        {
-            double acc[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { acc[i] = delta[0] + i; asm volatile("" : "+v"(acc[i])); }
-#pragma unroll
-            for (int i = 0; i < BR_EXP_VALU / 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(acc[j]));
-#pragma unroll
-            for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(acc[i]));
-        }
-#endif
-#ifdef BR_EXP_MEM   // experiment: BR_EXP_MEM columns (512 B each) of the saved J re-read per Newton iteration
-        {
-            const BR_GLOBAL double* jg = launder((const double*)Jsave);
-            double d[BR_EXP_MEM];
-#pragma unroll
-            for (int i = 0; i < BR_EXP_MEM; ++i) d[i] = jg[i * 64 * CPL + lane];
-#pragma unroll
-            for (int i = 0; i < BR_EXP_MEM; ++i) asm volatile("" :: "v"(d[i]));
-        }
-#endif
+        BR_X_AFTER_ITER();
         BR_CLK(c3);
         act_code = ctl_post_solve<CPL>(C, V, lane, delta, lu_fail);
         BR_ACC(cyc_ctl, c3);
@@ -1191,7 +1259,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
 #endif
         st[13] = ud(C->tn);
         st[16] = o.ign >= 0 ? ud(C->t_ign) : NAN; st[17] = o.ign >= 0 ? ud(C->ign_rate) : NAN;
-        st[18] = o.ign >= 0 ? ud(C->ign_dt) : NAN; st[19] = 0.0;
+        st[18] = o.ign >= 0 ? ud(C->ign_dt) : NAN; st[19] = st_in[7] + ui(C->nfe_dq);
     }
     }   // next reactor
 }
@@ -2077,7 +2145,7 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     const int rid = blockIdx.x;
     if (rid >= N) return;
     const int lane = threadIdx.x;
-    __shared__ double prow[64];
+    __shared__ double prow[256];
     double* Jt = ws + (size_t)rid * (NMAX * WAVE + lu_ws_doubles(NMAX));
     double* LU = Jt + NMAX * WAVE;
     for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
@@ -2087,10 +2155,14 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     // search + gather path), the second in the first one's pivot order (every pivot on its own lane:
     // the factors come out in step order, no gather); the solve uses the second one's factors
     int perm = lane;
-    int f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+    auto factor = [&]() {
+        if constexpr (NMAX > 32 && BR_LU_MFMA) return lu_factor_mf<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
+        else return lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+    };
+    int f = factor();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
-    f = lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+    f = factor();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     const double r = lu_solve<NMAX>(LU, n, lane, perm, lane < n ? b[(size_t)rid * n + lane] : 0.0, (LDSd*)prow);
@@ -2114,8 +2186,13 @@ __global__ __launch_bounds__(64) void k_lu_check2(int N, int n, const double* J,
         }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
+    // twice, as k_lu_check: natural order first (gather path), then the first one's pivot order
+    // (the no-gather path when every pivot stays on its position); the solve uses the second
     int perm[2] = {lane, lane + 64};
-    const int f = lu_factor2<NMAX>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
+    int f = lu_factor2<NMAX>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    f = lu_factor2<NMAX>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     double r[2];
@@ -2125,6 +2202,61 @@ __global__ __launch_bounds__(64) void k_lu_check2(int N, int n, const double* J,
     if (lane == 0) fail[rid] = f;
 }
 }  // namespace
+
+// diagnostic (not in brhip.h): the factor workspace [M | D^-1] and the step -> row map after one
+// (twice = 0) or two factorizations of I - gamma J, for checking the LU against a lane-level
+// emulation (scripts/emu/lu_mf_emu.py). J[N][n][n] row-major; F[N][lu_ws_doubles(nmax)], perm[N][64].
+namespace {
+template <int NMAX, int STOP>
+__global__ __launch_bounds__(64) void k_lu_factor_dbg(int N, int n, const double* J, const double* g, int twice,
+                                                      double* ws, double* Fout, int* pout) {
+    const int rid = blockIdx.x;
+    if (rid >= N) return;
+    const int lane = threadIdx.x;
+    __shared__ double scr[256];
+    double* Jt = ws + (size_t)rid * (NMAX * WAVE + lu_ws_doubles(NMAX));
+    double* LU = Jt + NMAX * WAVE;
+    for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
+    for (int i = lane; i < lu_ws_doubles(NMAX); i += 64) LU[i] = __builtin_nan("");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    int perm = lane;
+    for (int r = 0; r <= twice; ++r) {
+        if constexpr (NMAX > 32 && BR_LU_MFMA) lu_factor_mf<NMAX, STOP>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
+        else lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+    }
+    for (int i = lane; i < lu_ws_doubles(NMAX); i += 64) Fout[(size_t)rid * lu_ws_doubles(NMAX) + i] = LU[i];
+    pout[(size_t)rid * 64 + lane] = perm;
+}
+}  // namespace
+extern "C" int br_debug_lu_factor(int N, int n, const double* J, const double* gamma, int twice, int stop, double* F,
+                                  int* perm) {
+    if (N <= 0 || n <= 32 || n > 64) return fail_code_input();
+    const int nmax = n <= 56 ? 56 : 64;
+    const size_t lw = lu_ws_doubles(nmax);
+    double *dJ, *dg, *dws, *dF;
+    int* dp;
+    HIPCHK(hipMalloc(&dJ, (size_t)N * n * n * 8));
+    HIPCHK(hipMalloc(&dg, (size_t)N * 8));
+    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * WAVE + lw) * 8));
+    HIPCHK(hipMalloc(&dF, (size_t)N * lw * 8));
+    HIPCHK(hipMalloc(&dp, (size_t)N * 64 * 4));
+    HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, twice, dws, dF, dp); };
+    if (nmax == 56) {
+        if (stop == 0) go(k_lu_factor_dbg<56, 0>);
+        else if (stop == 1) go(k_lu_factor_dbg<56, 1>);
+        else go(k_lu_factor_dbg<56, (1 << 20)>);
+    } else go(k_lu_factor_dbg<64, (1 << 20)>);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(F, dF, (size_t)N * lw * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(perm, dp, (size_t)N * 64 * 4, hipMemcpyDeviceToHost));
+    hipFree(dJ); hipFree(dg); hipFree(dws); hipFree(dF); hipFree(dp);
+    return 0;
+}
 
 extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* gamma, const double* b, double* x,
                                  int* fail_out) {

@@ -1221,6 +1221,7 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
                     st[0] = (double)c.nst; st[1] = (double)c.nfe; st[2] = (double)c.nje; st[3] = (double)c.nsetups;
                     st[4] = (double)c.nni; st[5] = (double)c.ncfn; st[6] = (double)c.netf;
                     st[16] = c.t_ign; st[17] = c.ign_rate; st[18] = c.ign_dt;
+                    st[19] = o.dq_jac ? (double)c.nje * n : 0.0;   // nfe_dq
                 }
                 has = false;
             } else {                                         // no room: keep integrating here
@@ -1248,7 +1249,7 @@ __global__ __launch_bounds__(64) void k_lane(DevMech M, int N, const double* __r
 #endif
                 st[13] = c.tn;
                 st[16] = o.ign >= 0 ? c.t_ign : NAN; st[17] = o.ign >= 0 ? c.ign_rate : NAN;
-                st[18] = o.ign >= 0 ? c.ign_dt : NAN; st[19] = 0.0;
+                st[18] = o.ign >= 0 ? c.ign_dt : NAN; st[19] = o.dq_jac ? (double)c.nje * n : 0.0;   // nfe_dq
             }
             has = false;
         }

@@ -693,6 +693,14 @@ void copy_str(char* dst, size_t cap, const std::string& s) {
     std::memcpy(dst, s.data(), k);
     dst[k] = 0;
 }
+// a name from batch.xml into a fixed field: an error instead of a silent truncation (a truncated
+// species name would match nothing and drop its composition entry; a truncated path opens another
+// file)
+void copy_field(char* dst, size_t cap, const std::string& s, const char* what) {
+    if (s.size() >= cap) throw MechError(std::string(what) + " too long (" + std::to_string(s.size()) + " characters, at most " +
+                                         std::to_string(cap - 1) + ")");
+    copy_str(dst, cap, s);
+}
 
 }  // namespace
 
@@ -774,13 +782,12 @@ int br_read_batch_xml(const char* path, br_batch_input* b) {
     try {
         auto root = parse_xml(path);
         std::string t;
-        if (root->findtext("gas_mech", t) && !t.empty()) copy_str(b->gas_mech, sizeof(b->gas_mech), strip(t));
-        if (root->findtext("surface_mech", t) && !t.empty()) copy_str(b->surface_mech, sizeof(b->surface_mech), strip(t));
+        if (root->findtext("gas_mech", t) && !t.empty()) copy_field(b->gas_mech, sizeof(b->gas_mech), strip(t), "<gas_mech>");
+        if (root->findtext("surface_mech", t) && !t.empty()) copy_field(b->surface_mech, sizeof(b->surface_mech), strip(t), "<surface_mech>");
         if (root->findtext("gasphase", t) && !t.empty()) {
             std::string g;
             for (const auto& s : split_ws(t)) g += (g.empty() ? "" : " ") + s;
-            if (g.size() >= sizeof(b->gasphase)) throw MechError("<gasphase> too long");
-            copy_str(b->gasphase, sizeof(b->gasphase), g);
+            copy_field(b->gasphase, sizeof(b->gasphase), g, "<gasphase>");
         }
         struct { const char* tag; double* v; int* has; } num[] = {
             {"T", &b->T, &b->has_T}, {"p", &b->p, &b->has_p}, {"Asv", &b->Asv, &b->has_Asv}, {"time", &b->time, &b->has_time}};
@@ -794,7 +801,7 @@ int br_read_batch_xml(const char* path, br_batch_input* b) {
             if (kv.size() > BR_BATCH_MAXCOMP) throw MechError("too many composition entries");
             b->ncomp = (int)kv.size();
             for (size_t i = 0; i < kv.size(); ++i) {
-                copy_str(b->comp_names[i], sizeof(b->comp_names[i]), kv[i].first);
+                copy_field(b->comp_names[i], sizeof(b->comp_names[i]), kv[i].first, "composition species name");
                 b->comp_values[i] = kv[i].second;
             }
         }

@@ -19,7 +19,7 @@ from .mechanism import Mechanism
 
 STAT_FIELDS = ("nsteps", "nfe", "nje", "nsetups", "nni", "ncfn", "netf", "status", "cyc_total", "cyc_rhs",
                "cyc_jac", "cyc_lu", "cyc_sol", "t_end", "cyc_ctl", "cyc_clk", "t_ign", "ign_rate", "ign_dt",
-               "reserved")
+               "nfe_dq")
 IGNITION_MARKER = "OH"   # the reference golden's ignition marker: max dX_OH/dt
 
 
@@ -130,7 +130,7 @@ class Engine:
         and p_last the state and pressure of the step's last RHS evaluation (save_data semantics).
         With tout (ascending output times) the stats dict also carries "yout" [N, nout, n], the
         states at those times (CVODE CV_NORMAL output, the step sequence is unchanged).
-        dq_jacobian: CVODE's difference-quotient Jacobian (the reference's setting) in the lane engine."""
+        dq_jacobian: CVODE's difference-quotient Jacobian (the reference's setting), both engines."""
         u = np.array(np.atleast_2d(u0), dtype=np.float64, order="C")
         N = u.shape[0]
         T, A, tf = self._arr(T, N), self._arr(Asv, N), self._arr(tf, N)

@@ -105,9 +105,10 @@ typedef struct br_opts {
     double* yout;             /* [N][nout][n] states at tout (host memory for br_integrate,
                                  device memory for br_integrate_dev); rows with tout > tf are
                                  left untouched                                             */
-    int dq_jacobian;          /* 1: CVODE's dense difference-quotient Jacobian (the reference's
-                                 CVODE_BDF() setting) in the one-reactor-per-lane engine;
-                                 0 (default): the analytic Jacobian, as the wavefront engine */
+    int dq_jacobian;          /* 1: CVODE's dense difference-quotient Jacobian (cvLsDenseDQJac:
+                                 the reference's CVODE_BDF() setting, src/BatchReactor.jl:140,
+                                 :204), n extra RHS per Jacobian, in both engines (lane and
+                                 wavefront); 0 (default): the analytic Jacobian              */
 } br_opts;
 
 #define BR_NSTAT 20
@@ -122,7 +123,7 @@ typedef struct br_stats {     /* per reactor; counters as CVODE's, then device c
                                  dX_k/dt, k = br_opts.ignition_species (NaN if not tracked) */
     double ign_rate;          /* that largest dX_k/dt [1/s]                                */
     double ign_dt;            /* width of that step (the resolution of t_ign) [s]            */
-    double reserved;
+    double nfe_dq;            /* RHS evaluations of the DQ Jacobian (CVODE's nfeDQ; not in nfe) */
 } br_stats;
 
 int         br_version(void);

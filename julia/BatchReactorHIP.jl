@@ -61,7 +61,7 @@ BrOpts(; rtol=1e-6, atol=1e-10, max_steps=100_000, device=0, ignition_species=0)
 
 # br_stats rows of the [NSTAT x N] matrix returned below
 const STAT_FIELDS = (:nsteps, :nfe, :nje, :nsetups, :nni, :ncfn, :netf, :status, :cyc_total, :cyc_rhs, :cyc_jac,
-                     :cyc_lu, :cyc_sol, :t_end, :cyc_ctl, :cyc_clk, :t_ign, :ign_rate, :ign_dt, :reserved)
+                     :cyc_lu, :cyc_sol, :t_end, :cyc_ctl, :cyc_clk, :t_ign, :ign_rate, :ign_dt, :nfe_dq)
 
 last_error() = unsafe_string(ccall((:br_last_error, lib), Cstring, ()))
 check(rc) = rc == 0 || error("libbrhip error $rc: " * last_error())
@@ -138,22 +138,30 @@ function compile_mechanism(gas_mech::AbstractString, therm::AbstractString, surf
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:br_mech_parse, lib), Cint, (Cstring, Cstring, Cstring, Cstring, Cint, Ref{Ptr{Cvoid}}),
                 gas_mech, therm, surf_mech, gasphase, conv, h))
-    d = Ref{BrMechDesc}()
-    check(ccall((:br_host_mech_desc, lib), Cint, (Ptr{Cvoid}, Ref{BrMechDesc}), h[], d))
-    ng, ns, nrg, nrs = Int(d[].ng), Int(d[].ns), Int(d[].nrg), Int(d[].nrs)
-    buf = zeros(UInt8, 64)
-    names = String[]
-    for i in 0:(ng + ns - 1)
-        check(ccall((:br_host_mech_species, lib), Cint, (Ptr{Cvoid}, Cint, Ptr{UInt8}, Csize_t), h[], i, buf, 64))
-        push!(names, unsafe_string(pointer(buf)))
+    # every step after br_mech_parse may throw (check): free what exists so far, then rethrow
+    m = C_NULL
+    try
+        d = Ref{BrMechDesc}()
+        check(ccall((:br_host_mech_desc, lib), Cint, (Ptr{Cvoid}, Ref{BrMechDesc}), h[], d))
+        ng, ns, nrg, nrs = Int(d[].ng), Int(d[].ns), Int(d[].nrg), Int(d[].nrs)
+        buf = zeros(UInt8, 64)
+        names = String[]
+        for i in 0:(ng + ns - 1)
+            check(ccall((:br_host_mech_species, lib), Cint, (Ptr{Cvoid}, Cint, Ptr{UInt8}, Csize_t), h[], i, buf, 64))
+            push!(names, unsafe_string(pointer(buf)))
+        end
+        molwt = copy(unsafe_wrap(Array, d[].molwt, ng))
+        theta0 = zeros(ns)
+        check(ccall((:br_host_mech_theta0, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], theta0))
+        m = mech_create(d, device)
+        dm = DeviceMech(h[], m, Int(device), ng, ns, nrg, nrs, names, molwt, theta0)
+        finalizer(_free!, dm)
+        return dm
+    catch
+        m != C_NULL && ccall((:br_mech_destroy, lib), Cint, (Ptr{Cvoid},), m)
+        ccall((:br_host_mech_free, lib), Cint, (Ptr{Cvoid},), h[])
+        rethrow()
     end
-    molwt = copy(unsafe_wrap(Array, d[].molwt, ng))
-    theta0 = zeros(ns)
-    check(ccall((:br_host_mech_theta0, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], theta0))
-    m = mech_create(d, device)
-    dm = DeviceMech(h[], m, Int(device), ng, ns, nrg, nrs, names, molwt, theta0)
-    finalizer(_free!, dm)
-    return dm
 end
 
 # br_batch_input (br_read_batch_xml)

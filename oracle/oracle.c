@@ -1423,6 +1423,12 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
 
 int orc_integrate_batch(const orc_mech* m, int N, const double* T, const double* Asv, double* u,
                         const double* tf, const orc_opts* o, orc_stats* st, int nthreads) {
+    return orc_integrate_batch_out(m, N, T, Asv, u, tf, o, st, nthreads, 0, NULL, NULL);
+}
+
+int orc_integrate_batch_out(const orc_mech* m, int N, const double* T, const double* Asv, double* u,
+                            const double* tf, const orc_opts* o, orc_stats* st, int nthreads,
+                            int nout, const double* tout, double* yout) {
     int n = m->ng + m->ns;
     int bad = 0;
 #ifdef _OPENMP
@@ -1430,7 +1436,8 @@ int orc_integrate_batch(const orc_mech* m, int N, const double* T, const double*
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : bad)
 #endif
     for (int i = 0; i < N; ++i) {
-        int r = orc_integrate(m, T[i], Asv ? Asv[i] : 1.0, u + (size_t)i * n, tf[i], o, st ? &st[i] : NULL, NULL, NULL);
+        int r = integrate_impl(m, T[i], Asv ? Asv[i] : 1.0, u + (size_t)i * n, tf[i], o, st ? &st[i] : NULL, NULL, NULL,
+                               nout, tout, yout ? yout + (size_t)i * nout * n : NULL);
         if (r) bad++;
     }
     (void)nthreads;

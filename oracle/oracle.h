@@ -112,6 +112,10 @@ int  orc_integrate_out(const orc_mech* m, double T, double Asv, double* u, doubl
 int  orc_integrate_batch(const orc_mech* m, int N, const double* T, const double* Asv,
                          double* u, const double* tf, const orc_opts* o, orc_stats* st,
                          int nthreads);
+/* same, plus each reactor's states at the nout output times: yout[N][nout][n] */
+int  orc_integrate_batch_out(const orc_mech* m, int N, const double* T, const double* Asv,
+                             double* u, const double* tf, const orc_opts* o, orc_stats* st,
+                             int nthreads, int nout, const double* tout, double* yout);
 
 #ifdef __cplusplus
 }

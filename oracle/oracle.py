@@ -84,6 +84,9 @@ def lib():
         L.orc_integrate_batch.argtypes = [C.c_void_p, C.c_int, dp, dp, dp, dp, C.POINTER(Opts),
                                           C.POINTER(Stats), C.c_int]
         L.orc_integrate_batch.restype = C.c_int
+        L.orc_integrate_batch_out.argtypes = [C.c_void_p, C.c_int, dp, dp, dp, dp, C.POINTER(Opts),
+                                              C.POINTER(Stats), C.c_int, C.c_int, dp, dp]
+        L.orc_integrate_batch_out.restype = C.c_int
         _lib = L
     return _lib
 
@@ -192,7 +195,8 @@ class Mech:
         lib().orc_integrate_out(self.h, T, Asv, _p(u), tf, C.byref(o), C.byref(st), len(tout), _p(tout), _p(Y))
         return u, st.asdict(), Y
 
-    def integrate_batch(self, T, Asv, U0, tf, rtol=1e-6, atol=1e-10, analytic_jac=True, nthreads=0):
+    def integrate_batch(self, T, Asv, U0, tf, rtol=1e-6, atol=1e-10, analytic_jac=True, nthreads=0, tout=None):
+        """OpenMP ensemble; with `tout`, also returns the states there (Y[N][len(tout)][n])."""
         N = len(T)
         U = np.array(U0, dtype=np.float64, order="C").reshape(N, self.n)
         T = np.ascontiguousarray(T, dtype=np.float64)
@@ -200,5 +204,11 @@ class Mech:
         tf = np.ascontiguousarray(np.broadcast_to(tf, (N,)), dtype=np.float64)
         o = Opts(rtol, atol, int(analytic_jac), 100000, 0.0, 0.0, self.ign1)
         st = (Stats * N)()
-        bad = lib().orc_integrate_batch(self.h, N, _p(T), _p(Asv), _p(U), _p(tf), C.byref(o), st, nthreads)
-        return U, [s.asdict() for s in st], bad
+        if tout is None:
+            bad = lib().orc_integrate_batch(self.h, N, _p(T), _p(Asv), _p(U), _p(tf), C.byref(o), st, nthreads)
+            return U, [s.asdict() for s in st], bad
+        tout = np.ascontiguousarray(tout, dtype=np.float64)
+        Y = np.zeros((N, len(tout), self.n))
+        bad = lib().orc_integrate_batch_out(self.h, N, _p(T), _p(Asv), _p(U), _p(tf), C.byref(o), st, nthreads,
+                                            len(tout), _p(tout), _p(Y))
+        return U, [s.asdict() for s in st], bad, Y

@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
 import _pkgload  # noqa: E402
 import oracle  # noqa: E402
-from test_gpu_parity import OUT_T  # noqa: E402
+from parity_bands import OUT_T  # noqa: E402
 
 pkg = _pkgload.load()
 from batchreactor_amd import ensemble  # noqa: E402

@@ -180,43 +180,24 @@ def _global_err(X, Ut):
 
 # Per-reactor parity at default tolerances (rtol 1e-6, atol 1e-10, src/BatchReactor.jl:141,:210),
 # 0 -> 10 s through ignition, on a slice of the synthetic ensemble (bench inputs),
-# at fixed output times (CVODE CV_NORMAL output through br_opts.tout). The oracle runs the same
-# algorithm with the same Jacobian kind, so every difference is rounding. How far rounding alone moves
-# a CVODE trajectory was measured on the oracle itself (second run with u0 perturbed by 1e-15
-# relative, same metric, 32-128 reactors per case; scripts/diag_spread.py):
-#                     before 0.5 t_ign   0.5..2 t_ign   after 2 t_ign   steps per reactor   t_ign
-#   GRI (analytic J)      1e-10              1.2            1.6             16 %          0.01 step
-#   gas+surf (analytic)   0.66               76             1.1             13 %          1.6 steps
-#   surface (analytic)    0.17               -              -               18 %            -
-#   H2/O2 (DQ J)          4.4                75             2.7             27 %          1.6 steps
-#   H2/O2, DQ increments x (1 +- 1e-15)  4.4           73             2.4
-# (units: 1e-4 |u| + 100 atol). Bounds per reactor and output time, in the same units: before
-# ignition 1 (the north_star 1e-4 bar) with the analytic Jacobian (measured on the GPU: <= 3e-10)
-# and 30 with CVODE's DQ Jacobian (whose finite differences amplify rounding; the lane engine's DQ
-# mode measures 18.6 on one of 256 H2/O2 reactors, 4x the oracle's own DQ spread -- the DQ mode is
-# opt-in, br_opts.dq_jacobian); across the ignition front 300; after it 30. Ignition time within 2
-# widths of the ignition step; steps within 35 % per reactor and 3 % summed over the slice.
-OUT_T = np.concatenate([[1e-6, 1e-5, 1e-4], np.logspace(-3, 1, 25)])
-_BANDS = ((0.0, 0.5, 1.0), (0.5, 2.0, 300.0), (2.0, np.inf, 30.0))
-DQ_PRE_IGNITION_BOUND = 30.0
-
-
-def _band_errors(Yg, Yo, tign):
-    """max error (units of the 1e-4 band) per ignition band for one reactor"""
-    e = (np.abs(Yg - Yo) / (1e-4 * np.abs(Yo) + 100 * ATOL)).max(axis=1)
-    r = OUT_T / tign if tign == tign else np.zeros_like(OUT_T)
-    return [float(e[(r >= lo) & (r < hi)].max(initial=0.0)) for lo, hi, _ in _BANDS]
+# at fixed output times (CVODE CV_NORMAL output through br_opts.tout), against per-case bounds set
+# from the oracle's own rounding spread (tests/parity_bands.py, profiles/r04_parity_spread.json).
+from parity_bands import OUT_T, BOUNDS, band_errors as _band_errors  # noqa: E402
+_BANDS = ((0.0, 0.5, 1.0), (0.5, 2.0, 300.0), (2.0, np.inf, 30.0))   # coarse bounds of the dense-output edge test
 
 
 @pytest.mark.parametrize("case,N,dq", [("h2o2", 256, False), ("gri", 64, False), ("surf", 64, False),
-                                      ("gas_surf", 32, False), ("h2o2", 256, True)],
-                         ids=["h2o2", "gri", "surf", "gas_surf", "h2o2-dq"])
+                                      ("gas_surf", 32, False), ("h2o2", 256, True), ("gri", 32, True),
+                                      ("gas_surf", 16, True)],
+                         ids=["h2o2", "gri", "surf", "gas_surf", "h2o2-dq", "gri-dq", "gas_surf-dq"])
 def test_integrate_parity(pkg, orc, gpu, case, N, dq):
     """Every reactor: same status (Success), the same ignition time to within the width of the
-    ignition step (the marker's resolution), states at the 28 output times within the bands above,
-    the same step count to 35 % per reactor and 3 % over the slice (rounding changes step sequences).
-    Both engines use the analytic Jacobian by default; "h2o2-dq" runs the lane engine with CVODE's
-    DQ Jacobian (br_opts.dq_jacobian, the reference's setting) against the oracle's DQ run."""
+    ignition step (the marker's resolution), states at the 28 output times within the case's bounds
+    (tests/parity_bands.py: 2x the oracle's own rounding spread across and after the front), the same
+    step count to 35 % per reactor and 3 % over the slice (rounding changes step sequences).
+    Both engines use the analytic Jacobian by default; the "-dq" cases run CVODE's DQ Jacobian
+    (br_opts.dq_jacobian, the reference's setting: the lane engine for H2/O2, the wavefront engine
+    for GRI and gas+surface) against the oracle's DQ run."""
     from batchreactor_amd import ensemble
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
@@ -226,7 +207,7 @@ def test_integrate_parity(pkg, orc, gpu, case, N, dq):
     assert np.all(st["status"] == 0), np.unique(st["status"])
     worst = np.zeros(3)
     nst_o = 0
-    bands = _BANDS if analytic else ((0.0, 0.5, DQ_PRE_IGNITION_BOUND),) + _BANDS[1:]
+    bounds = BOUNDS[(case, dq)]
     for i in range(N):
         uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], 10.0, OUT_T, analytic_jac=analytic)
         assert so["status"] == 0
@@ -236,19 +217,24 @@ def test_integrate_parity(pkg, orc, gpu, case, N, dq):
                 (case, i, st["t_ign"][i], ti, st["ign_dt"][i], so["ign_dt"])
         eb = _band_errors(st["yout"][i], Yo, ti)
         worst = np.maximum(worst, eb)
-        for (lo, hi, bound), e in zip(bands, eb):
-            assert e <= bound, (case, i, (lo, hi), e)
+        for w, (bound, e) in enumerate(zip(bounds, eb)):
+            assert e <= bound, (case, dq, i, ("pre", "front", "post")[w], e, bound)
         assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.35 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
         nst_o += so["nsteps"]
     assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
-    print(f"\n  {case}{' (DQ)' if dq else ''}: worst error per band (units of 1e-4|u|+1e-8): {worst}")
+    if dq:
+        assert np.all(st["nfe_dq"] == st["nje"] * pm.n), "DQ Jacobian: n RHS per Jacobian"
+    print(f"\n  {case}{' (DQ)' if dq else ''}: worst error per band (units of 1e-4|u|+1e-8): {worst}, bounds {bounds}")
 
 
-def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu):
+@pytest.mark.parametrize("dq", [False, True], ids=["analytic", "dq"])
+def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu, dq):
     """The HIP engine on the reference's own gas+surf case (test/batch_gas_and_surf: GRI + ch4ni,
     T = 1173 K, Asv = 1, rtol 1e-6 / atol 1e-10): ignition (max dX_OH/dt, br_stats.t_ign) at the
-    golden's 3.8109e-3 s to 1e-3, and every committed golden row (state at the same time through
-    br_opts.tout) within the per-window bounds the oracle is held to (tests/test_oracle.py)."""
+    golden's 3.8109e-3 s to 1e-3, the golden's accepted-step count (1,918) to 10 %, and every
+    committed golden row (state at the same time through br_opts.tout) within the per-window bounds
+    the oracle is held to (tests/test_oracle.py). "dq": the wavefront engine with CVODE's DQ
+    Jacobian, the reference's own setting (src/BatchReactor.jl:204-210)."""
     import csv
     import json
     from conftest import GOLDEN
@@ -265,8 +251,10 @@ def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu):
     x = pm.mole_fractions({"CH4": 0.25, "O2": 0.5, "N2": 0.25})
     u0 = pm.initial_state(1173.0, 1e5, x)
     tg = g[:, 0]
-    U, st = pkg.Engine(pm).integrate([1173.0], [1.0], u0[None, :], 10.0, tout=tg)
+    U, st = pkg.Engine(pm).integrate([1173.0], [1.0], u0[None, :], 10.0, tout=tg, dq_jacobian=dq)
     assert st["status"][0] == 0
+    print(f"\n  golden gas+surf ({'DQ' if dq else 'analytic'} J): {int(st['nsteps'][0])} steps "
+          f"(golden {meta['accepted_steps']}), t_ign {st['t_ign'][0]:.6e}")
     assert abs(st["t_ign"][0] / meta["t_ign_max_dXOH_dt"] - 1) < 1e-3, st["t_ign"][0]
     assert abs(st["nsteps"][0] / meta["accepted_steps"] - 1) < 0.1
     Y = st["yout"][0]

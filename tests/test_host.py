@@ -271,6 +271,23 @@ def test_native_batch_xml(pkg, case):
     assert comp == d["molefractions"] and b.comp_is_mass == 0
 
 
+@pytest.mark.parametrize("field", ["species", "gas_mech"])
+def test_native_batch_xml_overlong_name(pkg, tmp_path, field):
+    """A name that does not fit its br_batch_input field is an input error, not a silent
+    truncation (a truncated species name would drop its composition entry)."""
+    long = "X" * 300
+    sp = long if field == "species" else "CH4"
+    gm = long if field == "gas_mech" else "grimech.dat"
+    p = tmp_path / "batch.xml"
+    p.write_text(f"<batch><gas_mech>{gm}</gas_mech><gasphase>CH4 O2 N2</gasphase>"
+                 f"<molefractions>{sp}=0.25,O2=0.5,N2=0.25</molefractions>"
+                 "<T>1173</T><p>1e5</p><time>10</time></batch>")
+    L = pkg._lib.lib()
+    b = pkg._lib.BatchInput()
+    assert L.br_read_batch_xml(str(p).encode(), ctypes.byref(b)) == -10
+    assert "too long" in L.br_last_error().decode()
+
+
 def test_cli_julia_string_format(pkg):
     """brhip_batch (the C-ABI-only batch_reactor program) formats CSV numbers as Julia's
     string(::Float64): every number token of the reference's own gas+surf CSVs comes back verbatim."""
