@@ -1006,7 +1006,13 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL>& V, int lane, dou
 #define BR_WPE 2
 #endif
 #ifndef BR_LU_MFMA
-#define BR_LU_MFMA 1   // 32 < NMAX <= 64: blocked LU with MFMA trailing updates (lu_factor_mf)
+// 32 < NMAX <= 64: 1 = blocked LU with fp64 MFMA trailing updates (lu_factor_mf) in the integrator;
+// 0 (default) = the row-per-lane VALU LU. Measured in-engine on GRI (round 4,
+// profiles/r04_lu_mfma_ab.json): MFMA 88.8k (panel 8) / 92.0k (panel 16) vs VALU 110.5k reactors/s --
+// the trailing matrix streams through the workspace (writes 6.6 -> 17 MB per reactor, wave time
+// parked in s_waitcnt 7.7 -> 13.6 M cycles) and costs more than the 12 % of VALU it saves.
+// lu_factor_mf stays built and tested (br_debug_lu_solve_mf).
+#define BR_LU_MFMA 0
 #endif
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
@@ -2139,7 +2145,7 @@ int br_integrate_multi(br_mech* const* mechs, int ndev, int N, const double* T, 
 // solve one right-hand side per matrix. J[N][n][n] row-major, b/x [N][n].
 // ------------------------------------------------------------------------------------
 namespace {
-template <int NMAX>
+template <int NMAX, bool MF = (NMAX > 32 && BR_LU_MFMA)>
 __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, const double* g, const double* b,
                                                  double* x, double* ws, int* fail) {
     const int rid = blockIdx.x;
@@ -2156,7 +2162,7 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     // the factors come out in step order, no gather); the solve uses the second one's factors
     int perm = lane;
     auto factor = [&]() {
-        if constexpr (NMAX > 32 && BR_LU_MFMA) return lu_factor_mf<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
+        if constexpr (MF) return lu_factor_mf<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
         else return lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
     };
     int f = factor();
@@ -2222,8 +2228,7 @@ __global__ __launch_bounds__(64) void k_lu_factor_dbg(int N, int n, const double
     __syncthreads();
     int perm = lane;
     for (int r = 0; r <= twice; ++r) {
-        if constexpr (NMAX > 32 && BR_LU_MFMA) lu_factor_mf<NMAX, STOP>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
-        else lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
+        lu_factor_mf<NMAX, STOP>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
     }
@@ -2278,6 +2283,31 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     else if (nmax == 56) hipLaunchKernelGGL(k_lu_check<56>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
     else if (nmax == 64) hipLaunchKernelGGL(k_lu_check<64>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
     else hipLaunchKernelGGL(k_lu_check2<72>, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(x, dx, (size_t)N * n * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));
+    hipFree(dJ); hipFree(dg); hipFree(db); hipFree(dx); hipFree(dws); hipFree(df);
+    return 0;
+}
+
+// diagnostic (not in brhip.h): br_debug_lu_solve with the MFMA-blocked LU (lu_factor_mf), 32 < n <= 64
+extern "C" int br_debug_lu_solve_mf(int N, int n, const double* J, const double* gamma, const double* b, double* x,
+                                    int* fail_out) {
+    if (N <= 0 || n <= 32 || n > 64) return fail_code_input();
+    const int nmax = n <= 56 ? 56 : 64;
+    double *dJ, *dg, *db, *dx, *dws;
+    int* df;
+    HIPCHK(hipMalloc(&dJ, (size_t)N * n * n * 8));
+    HIPCHK(hipMalloc(&dg, (size_t)N * 8));
+    HIPCHK(hipMalloc(&db, (size_t)N * n * 8));
+    HIPCHK(hipMalloc(&dx, (size_t)N * n * 8));
+    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
+    HIPCHK(hipMalloc(&df, (size_t)N * 4));
+    HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(db, b, (size_t)N * n * 8, hipMemcpyHostToDevice));
+    if (nmax == 56) hipLaunchKernelGGL((k_lu_check<56, true>), dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
+    else hipLaunchKernelGGL((k_lu_check<64, true>), dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(x, dx, (size_t)N * n * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));

@@ -142,10 +142,10 @@ def main():
     alg_bytes = N * 8.0 * ((3 + mech.n) + (mech.n + pkg._lib.NSTAT))
 
     # measured memory-side bytes per reactor of this kernel at this HEAD (rocprofv3 FETCH_SIZE x2
-    # + WRITE_SIZE passes, scripts/pmc_traffic.py -> profiles/r03_traffic_<config>.json)
+    # + WRITE_SIZE passes, scripts/pmc_traffic.py -> profiles/r04_traffic_<config>.json)
     traffic, traffic_src = None, None
     tpath = None
-    for rnd in ("r03", "r02"):   # the newest round's summary
+    for rnd in ("r04", "r03", "r02"):   # the newest round's summary
         cand = os.path.join(ROOT, "profiles", f"{rnd}_traffic_{args.config}.json")
         if os.path.exists(cand):
             tpath = cand
@@ -174,7 +174,7 @@ def main():
     cpu = parity = phases = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, parity = cpu_baseline(mech, args.config, T, Asv, U0, tf, dU.cpu().numpy(), stats["status"],
-                                   args.cpu_seconds)
+                                   args.cpu_seconds, eng)
     if rank == 0 and world == 1 and not args.no_phase:
         phases = run_phase_split(args.config)
 
@@ -290,12 +290,16 @@ def phase_split(args):
     print(json.dumps(out))
 
 
-def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
+def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds, eng):
     """The C CPU oracle (CVODE restatement, analytic Jacobian, OpenMP over reactors) on a bounded
     sample of the same workload, all threads and one thread; also checks the GPU results of that
-    sample against it (per reactor, the metric of tests/test_gpu_parity.py at t = tf)."""
+    sample against it: per reactor at t = tf, and per ignition window at the 28 output times of
+    tests/test_gpu_parity.py against that test's per-case bounds (tests/parity_bands.py; the GPU
+    states there come from one more, untimed integration of the sample with dense output)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle
+    import parity_bands as PB
     cfg = CONFIGS[config]
     lib = os.path.join(ROOT, "tests", "golden", "lib")
     om = oracle.Mech(os.path.join(lib, cfg["gas"]) if cfg["gas"] else None, os.path.join(lib, "therm.dat"),
@@ -309,8 +313,9 @@ def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
     dt = time.perf_counter() - t0
     per = dt / k * threads
     k = int(max(k, min(len(T), seconds / max(per, 1e-6) * threads)))
-    t0 = time.perf_counter()
-    Uo, sto, bad = om.integrate_batch(T[:k], Asv[:k], U0[:k], tf[:k], analytic_jac=True, nthreads=threads)
+    t0 = time.perf_counter()   # (dense output at the test's 28 times: the same step sequence)
+    Uo, sto, bad, Yo = om.integrate_batch(T[:k], Asv[:k], U0[:k], tf[:k], analytic_jac=True, nthreads=threads,
+                                          tout=PB.OUT_T)
     dt = time.perf_counter() - t0
     k1 = int(max(1, min(k, 0.25 * seconds / max(per, 1e-6))))      # single thread, a quarter of the budget
     t1 = time.perf_counter()
@@ -324,6 +329,18 @@ def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds):
                "reactors": int(ok.sum()), "failed_either": int((~ok).sum()), "median": float(np.median(err)),
                "p99": float(np.percentile(err, 99)), "max": float(err.max()),
                "frac_le_1": float(np.mean(err <= 1.0)), "frac_le_30": float(np.mean(err <= 30.0))}
+        # per ignition window, the test's metric and bounds (the bench integrates with the analytic J)
+        _, stg = eng.integrate(T[:k], Asv[:k], U0[:k], tf[:k], tout=PB.OUT_T)
+        okw = ok & (stg["status"] == 0)
+        W = np.array([PB.band_errors(stg["yout"][i], Yo[i], sto[i]["t_ign"]) for i in np.nonzero(okw)[0]])
+        bnd = PB.BOUNDS[(config, False)]
+        rel["windows"] = {
+            "metric": "max over the 28 output times of tests/test_gpu_parity.py in each window of t/t_ign "
+                      "(pre < 0.5, front 0.5..2, post >= 2) of max_k |Y_gpu-Y_orc| / (1e-4 |Y_orc| + 100 atol)",
+            "reactors": int(okw.sum()), "bounds": list(bnd[:3]),
+            "max": W.max(0).tolist(), "p99": np.percentile(W, 99, axis=0).tolist(),
+            "median": np.median(W, axis=0).tolist(),
+            "frac_within_bounds": float(np.mean(np.all(W <= np.array(bnd[:3]), axis=1)))}
     else:
         rel = None
     return ({"value": k / dt, "unit": "reactors/s", "cores": threads, "kind": "port",

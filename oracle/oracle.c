@@ -601,6 +601,18 @@ static void falloff(const orc_mech* m, const grxn_t* r, const tcache_t* c, int i
     *dfac = (F / ((1 + Pr) * (1 + Pr)) + F * g / (1 + Pr)) * (k0 / kinf);
 }
 
+/* diagnostic hook (scripts/diag_spread.py): every rate of progress times (1 +- eps), the sign from a
+ * hash of (call, reaction) -- the few-ulp differences of an RHS implementation that evaluates the
+ * same formulas in another order, amplified by CVODE's DQ Jacobian (inc ~ 1e-8 |y|). 0 = off. */
+static double g_rop_jitter = 0.0;
+static unsigned long long g_rop_calls = 0;
+void orc_set_rop_jitter(double eps) { g_rop_jitter = eps; }
+static inline double rop_jit(int i) {
+    unsigned long long h = (g_rop_calls * 0x9E3779B97F4A7C15ull) ^ ((unsigned long long)i * 0xC2B2AE3D27D4EB4Full);
+    h ^= h >> 31;
+    return (h & 1) ? g_rop_jitter : -g_rop_jitter;
+}
+
 /* gas rates of progress q[nrg] from concentrations c[ng] */
 static void gas_rop(const orc_mech* m, const tcache_t* tc, const double* c, double* q) {
     for (int i = 0; i < m->nrg; ++i) {
@@ -619,8 +631,9 @@ static void gas_rop(const orc_mech* m, const tcache_t* tc, const double* c, doub
                 if (m->conv & ORC_CONV_FALLOFF_XM) D *= Mc * 1e-6;   /* [M] in mol/cm3 */
             }
         }
-        q[i] = D;
+        q[i] = g_rop_jitter != 0.0 ? D * (1.0 + rop_jit(i)) : D;
     }
+    g_rop_calls++;
 }
 
 static void surf_rop(const orc_mech* m, const tcache_t* tc, const double* c, const double* th, double* q) {
@@ -640,8 +653,9 @@ static void surf_rop(const orc_mech* m, const tcache_t* tc, const double* c, con
             if (s < m->ng) P *= c[s];
             else P *= r->stick ? th[s - m->ng] : th[s - m->ng] * G / m->sigma[s];
         }
-        q[i] = k * P;
+        q[i] = g_rop_jitter != 0.0 ? k * P * (1.0 + rop_jit(100000 + i)) : k * P;
     }
+    g_rop_calls++;
 }
 
 static void conc_from_x(const orc_mech* m, double T, double p, const double* x, double* c) {

@@ -108,6 +108,8 @@ int  orc_integrate(const orc_mech* m, double T, double Asv, double* u, double tf
 /* same, plus the state at nout ascending output times (CV_NORMAL + CVodeGetDky); yout[nout][n] */
 int  orc_integrate_out(const orc_mech* m, double T, double Asv, double* u, double tf, const orc_opts* o,
                        orc_stats* st, int nout, const double* tout, double* yout);
+/* diagnostic: perturb every rate of progress by a relative +-eps (0 = off; not thread-safe) */
+void orc_set_rop_jitter(double eps);
 /* ensemble (OpenMP over reactors): u[N][n] row per reactor */
 int  orc_integrate_batch(const orc_mech* m, int N, const double* T, const double* Asv,
                          double* u, const double* tf, const orc_opts* o, orc_stats* st,

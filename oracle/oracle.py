@@ -87,6 +87,8 @@ def lib():
         L.orc_integrate_batch_out.argtypes = [C.c_void_p, C.c_int, dp, dp, dp, dp, C.POINTER(Opts),
                                               C.POINTER(Stats), C.c_int, C.c_int, dp, dp]
         L.orc_integrate_batch_out.restype = C.c_int
+        L.orc_set_rop_jitter.argtypes = [C.c_double]
+        L.orc_set_rop_jitter.restype = None
         _lib = L
     return _lib
 

@@ -10,6 +10,9 @@ from batchreactor_amd import ensemble
 from parity_bands import OUT_T, band_errors as _band_errors
 LIB=os.path.join(ROOT, 'tests', 'golden', 'lib')
 case=sys.argv[1]; N=int(sys.argv[2]); aj=int(sys.argv[3])
+# ORC_ROP_JITTER=<eps>: the perturbed run also evaluates every rate of progress with a relative +-eps
+# (an RHS implementation that rounds differently; what CVODE's DQ Jacobian is most sensitive to)
+ROPJ=float(os.environ.get('ORC_ROP_JITTER','0'))
 gas={'h2o2':'h2o2.dat','gri':'grimech.dat','gas_surf':'grimech.dat','surf':None}[case]
 surf='ch4ni.xml' if case in ('gas_surf','surf') else None
 SG="CH4 H2O H2 CO CO2 O2 N2".split()
@@ -21,7 +24,9 @@ W=[];S=[];dti=[];nfail=0
 for i in range(N):
     ua,sa,Ya=om.integrate_out(T[i],Asv[i],U0[i],10.0,OUT_T,analytic_jac=bool(aj))
     up=U0[i]*(1+1e-15*rng.standard_normal(len(U0[i])))
+    orc.lib().orc_set_rop_jitter(ROPJ)
     ub,sb,Yb=om.integrate_out(T[i],Asv[i],up,10.0,OUT_T,analytic_jac=bool(aj))
+    orc.lib().orc_set_rop_jitter(0.0)
     if sa['status'] != 0 or sb['status'] != 0:   # a CVODE failure in one run (rounding-chaotic: C5 -3)
         nfail += 1
         continue
@@ -30,7 +35,7 @@ for i in range(N):
 W=np.array(W); S=np.array(S)
 print(case,'aj',aj,'band max',W.max(0),'p99',np.percentile(W,99,axis=0),'steps rel max',np.abs(S).max(),'p90',np.percentile(np.abs(S),90),'sum',S.mean(),'tign/dt max',max(dti) if dti else None,'failed pairs',nfail)
 import json
-print('JSON', json.dumps({'case': case, 'analytic_jac': bool(aj), 'reactors': N, 'excluded_failed_pairs': nfail,
+print('JSON', json.dumps({'case': case, 'analytic_jac': bool(aj), 'reactors': N, 'rop_jitter': ROPJ, 'dq_inc_jitter': float(os.environ.get('ORC_DQ_JITTER','0')), 'excluded_failed_pairs': nfail,
                           'band_max': W.max(0).tolist(), 'band_p99': np.percentile(W, 99, axis=0).tolist(),
                           'steps_rel_max': float(np.abs(S).max()), 'steps_rel_p90': float(np.percentile(np.abs(S), 90)),
                           'tign_over_dt_max': float(max(dti)) if dti else None}))

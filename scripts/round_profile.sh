@@ -1,6 +1,6 @@
 #!/bin/bash
 # Refresh the judged measurement files at this HEAD (one GPU session):
-#  1. PMC traffic per config (scripts/pmc_all.sh) -> profiles/r03_traffic_<cfg>.json (bench reads it)
+#  1. PMC traffic per config (scripts/pmc_all.sh) -> profiles/${TAG}_traffic_<cfg>.json (bench reads it)
 #  2. one full bench line per config (CPU leg + phase split) -> profiles/${TAG}_bench_<cfg>.json
 #  3. rocprofv3 --kernel-trace --stats of the default (GRI) bench -> profiles/${TAG}_gri1e5_kernel_stats.csv
 # Stops at the first step that fails, times out or faults. Only gpurun_out/ comes back from a GPU box:
@@ -8,12 +8,13 @@
 # cp gpurun_out/profiles/* profiles/).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
+export TAG
 mkdir -p gpurun_out/profiles profiles
 CFGS=${CFGS:-gri h2o2 surf gas_surf}
 if [ -z "$NO_PMC" ]; then
   bash scripts/pmc_all.sh $CFGS || exit $?
-  for c in $CFGS; do cp gpurun_out/r03_traffic_$c.json profiles/r03_traffic_$c.json; cp gpurun_out/r03_traffic_$c.json gpurun_out/profiles/; done
+  for c in $CFGS; do cp gpurun_out/${TAG}_traffic_$c.json profiles/${TAG}_traffic_$c.json; cp gpurun_out/${TAG}_traffic_$c.json gpurun_out/profiles/; done
 fi
 for c in $CFGS; do
   timeout -k 10 400 python3 bench.py --config $c > gpurun_out/bench_$c.log 2>&1 || { echo "bench $c failed"; tail -5 gpurun_out/bench_$c.log; exit 1; }

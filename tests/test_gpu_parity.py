@@ -213,18 +213,18 @@ def test_integrate_parity(pkg, orc, gpu, case, N, dq):
         assert so["status"] == 0
         ti = so["t_ign"]
         if pm.ng > 7:   # gas-phase mechanisms carry the OH marker; it resolves ignition to one step
-            assert abs(st["t_ign"][i] - ti) <= 2 * max(st["ign_dt"][i], so["ign_dt"]) + 1e-4 * ti, \
+            assert abs(st["t_ign"][i] - ti) <= bounds[3] * max(st["ign_dt"][i], so["ign_dt"]) + 1e-4 * ti, \
                 (case, i, st["t_ign"][i], ti, st["ign_dt"][i], so["ign_dt"])
         eb = _band_errors(st["yout"][i], Yo, ti)
         worst = np.maximum(worst, eb)
-        for w, (bound, e) in enumerate(zip(bounds, eb)):
+        for w, (bound, e) in enumerate(zip(bounds[:3], eb)):
             assert e <= bound, (case, dq, i, ("pre", "front", "post")[w], e, bound)
         assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.35 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
         nst_o += so["nsteps"]
     assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
     if dq:
         assert np.all(st["nfe_dq"] == st["nje"] * pm.n), "DQ Jacobian: n RHS per Jacobian"
-    print(f"\n  {case}{' (DQ)' if dq else ''}: worst error per band (units of 1e-4|u|+1e-8): {worst}, bounds {bounds}")
+    print(f"\n  {case}{' (DQ)' if dq else ''}: worst error per band (units of 1e-4|u|+1e-8): {worst}, bounds {bounds[:3]}")
 
 
 @pytest.mark.parametrize("dq", [False, True], ids=["analytic", "dq"])
@@ -238,7 +238,7 @@ def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu, dq):
     import csv
     import json
     from conftest import GOLDEN
-    from test_oracle import _WINDOWS
+    from test_oracle import _WINDOWS, _WINDOWS_ADMISSIBLE
 
     def golden(name):
         rows = list(csv.reader(open(os.path.join(GOLDEN, name))))
@@ -263,24 +263,29 @@ def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu, dq):
     ex = np.where(np.abs(G) >= 1e-4, np.abs(X - G) / np.maximum(np.abs(G), 1e-300), 0.0).max(axis=1)
     S = s[:, 2:]
     es = np.where(np.abs(S) >= 1e-4, np.abs(Y[:, pm.ng:] - S) / np.maximum(np.abs(S), 1e-300), 0.0).max(axis=1)
-    for lo, hi, tol, tolc in _WINDOWS:
+    for lo, hi, tol, tolc in (_WINDOWS_ADMISSIBLE if dq else _WINDOWS):
         sel = (tg >= lo) & (tg < hi)
         assert ex[sel].max() < tol and es[sel].max() < tolc, (lo, hi, ex[sel].max(), es[sel].max())
 
 
-@pytest.mark.parametrize("case,N", [("h2o2", 16), ("gri", 4), ("surf", 8), ("gas_surf", 2)])
-def test_integrate_parity_tight(pkg, orc, gpu, case, N):
+@pytest.mark.parametrize("case,N,dq", [("h2o2", 16, False), ("gri", 4, False), ("surf", 8, False),
+                                      ("gas_surf", 2, False), ("gri", 4, True), ("gas_surf", 2, True)],
+                         ids=["h2o2", "gri", "surf", "gas_surf", "gri-dq", "gas_surf-dq"])
+def test_integrate_parity_tight(pkg, orc, gpu, case, N, dq):
     """Tight tolerances (rtol 1e-10, atol 1e-16) on both sides: the two integrations converge to the
     same trajectory, so the end states (tf = 1e-2 s, through ignition for the gas cases) must agree
-    to 1e-6 relative (absolute floor 1e-14 kg/m3)."""
+    to 1e-6 relative (absolute floor 1e-14 kg/m3). "-dq": both with CVODE's DQ Jacobian (the
+    wavefront engine's dq_jacobian path against the oracle's cvLsDenseDQJac)."""
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
     T, Asv, U0 = _ignition_inputs(pm, case, N, 6)
     tf = 1e-2
-    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16)
+    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16, dq_jacobian=dq)
     assert np.all(st["status"] == 0)
+    if dq:
+        assert np.all(st["nfe_dq"] == st["nje"] * pm.n)
     for i in range(N):
-        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf, analytic_jac=True, rtol=1e-10, atol=1e-16)
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf, analytic_jac=not dq, rtol=1e-10, atol=1e-16)
         assert so["status"] == 0
         e = close_states(U[i], uo, rtol=1e-6, floor=1e-14)
         assert e <= 1.0, (case, i, e)
@@ -335,6 +340,32 @@ def test_batched_lu_solve(pkg, gpu, n):
     L = pkg._lib.lib()
     rc = L.br_debug_lu_solve(N, n, pkg._lib.dptr(J), pkg._lib.dptr(g), pkg._lib.dptr(b), pkg._lib.dptr(x),
                              f.ctypes.data_as(C.POINTER(C.c_int)))
+    assert rc == 0 and np.all(f == 0)
+    for i in range(N):
+        A = np.eye(n) - g[i] * J[i]
+        res = A @ x[i] - b[i]
+        assert np.max(np.abs(res)) <= 1e-12 * (np.abs(A).sum(1).max() * np.abs(x[i]).max() + np.abs(b[i]).max())
+
+
+@pytest.mark.parametrize("n", [33, 53, 64])
+def test_batched_lu_solve_mfma(pkg, gpu, n):
+    """The MFMA-blocked LU (lu_factor_mf: 8-column panels, trailing updates X += E' X[piv] on
+    v_mfma_f64_16x16x4f64; not the integrator's default, see profiles/r04_lu_mfma_ab.json) + solve,
+    the same matrices and backward-error bound as test_batched_lu_solve; factored twice (natural
+    row order, then the first factorization's pivot order)."""
+    import ctypes as C
+    rng = np.random.default_rng(n)
+    N = 64
+    J = rng.standard_normal((N, n, n)) * np.exp(rng.uniform(-8, 8, (N, n, 1)))
+    g = np.exp(rng.uniform(-12, -2, N))
+    b = rng.standard_normal((N, n))
+    x = np.zeros((N, n))
+    f = np.zeros(N, np.int32)
+    L = pkg._lib.lib()
+    fn = L.br_debug_lu_solve_mf
+    fn.restype = C.c_int
+    rc = fn(N, n, pkg._lib.dptr(J), pkg._lib.dptr(g), pkg._lib.dptr(b), pkg._lib.dptr(x),
+            f.ctypes.data_as(C.POINTER(C.c_int)))
     assert rc == 0 and np.all(f == 0)
     for i in range(N):
         A = np.eye(n) - g[i] * J[i]

@@ -216,6 +216,12 @@ def test_golden_ignition_time(orc, gs_ref):
 # moves the steep species by a few percent)
 _WINDOWS = [(0.0, 1e-3, 1e-5, 2e-4), (1e-3, 3.7e-3, 3e-3, 3e-3), (3.7e-3, 3.95e-3, 6e-2, 1e-2),
             (3.95e-3, 10.01, 9e-4, 8e-4)]
+# The admissible bound of each window (test_golden_window_bounds_derived): the golden's own global
+# error plus a rtol 1e-6 run's, i.e. how far two correct CVODE runs of this case may sit apart
+# without any model difference (pre-ignition at least the north_star's 1e-4). A run whose step
+# sequence is rounding-chaotic (CVODE's DQ Jacobian on the GPU, tests/parity_bands.py) is held to these.
+_WINDOWS_ADMISSIBLE = [(0.0, 1e-3, 1e-4, 3.7e-4), (1e-3, 3.7e-3, 4e-3, 5.9e-3), (3.7e-3, 3.95e-3, 0.11, 1.4e-2),
+                       (3.95e-3, 10.01, 9.7e-4, 8.9e-4)]
 
 
 def test_golden_all_rows_scored(orc, gs_ref, capsys):
@@ -281,5 +287,9 @@ def test_golden_window_bounds_derived(orc, gs_ref, capsys):
                      f"{c_meas[sel].max():.2e}, bound {tolc:g}")
         assert e_meas[sel].max() <= tol <= adm, lines[-1]
         assert c_meas[sel].max() <= tolc <= admc, lines[-1]
+    for lo, hi, tol, tolc in _WINDOWS_ADMISSIBLE:   # the admissible constants are what this derivation gives
+        sel = (tg >= lo) & (tg < hi)
+        assert tol <= max(1e-4, e_gold[sel].max() + e_orc[sel].max()), (lo, hi, tol)
+        assert tolc <= max(1e-4, c_gold[sel].max() + c_orc[sel].max()), (lo, hi, tolc)
     with capsys.disabled():
         print("\n  golden window bounds (converged oracle run, rtol 1e-10):\n    " + "\n    ".join(lines))
