@@ -118,17 +118,17 @@ __host__ __device__ inline int vec_bytes(int cpl) {
 // Nordsieck / work vectors in the reactor's LDS block: V.at(vec, s) = component lane + 64 s of
 // vector vec. (Register-resident vectors stored to LDS around each Newton setup measured GRI
 // -1.1 %, surf -11 % in round 2: the extra VGPRs cost occupancy.)
-template <int CPL>
+template <int CPL, int GW = 64>
 struct VA {
     typedef __attribute__((address_space(3))) double LD;
     LD* p;
     int lane;
     __device__ __forceinline__ LD& at(int j, int s) const {
-        if (CPL == 1 || s == 0) return p[j * 64 + lane];
+        if (CPL == 1 || s == 0) return p[j * GW + lane];
         return p[V1OFF + 8 * j + (lane < 8 ? lane : 72 + lane)];
     }
 };
-template <int CPL> using VT = VA<CPL>;
+template <int CPL, int GW = 64> using VT = VA<CPL, GW>;
 // component slot s's value of vector j for a uniform j in [0, QMAX + 1] (register arrays cannot be
 // indexed dynamically: a select chain, scalar branches on the uniform j)
 template <int CPL, class V_>
@@ -199,6 +199,42 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
 // surface-only +2.7 %, round 3)
 __device__ __forceinline__ double ud(const LDbl& x) { return (double)x; }
 __device__ __forceinline__ int ui(const __attribute__((address_space(3))) int& x) { return uni((int)x); }
+// Reactor groups: the wavefront engine runs one reactor per wave (group width GW = 64); the quad
+// engine (brhip_quad.hpp) four per wave, one per 16-lane DPP row (GW = 16), with `lane` the lane
+// within the group. The controller's values are uniform per group: scalar for GW = 64
+// (readfirstlane: SGPRs, scalar branches), per-lane VGPRs with exec-masked branches for GW = 16;
+// reductions and broadcasts over the group (DPP row butterflies, ds_bpermute inside the row).
+template <int GW>
+__device__ __forceinline__ int gui(const __attribute__((address_space(3))) int& x) {
+    if constexpr (GW == 64) return uni((int)x);
+    else return (int)x;
+}
+template <int GW>
+__device__ __forceinline__ int guni(int v) {
+    if constexpr (GW == 64) return uni(v);
+    else return v;
+}
+template <int GW>
+__device__ __forceinline__ double guni(double v) {
+    if constexpr (GW == 64) return uni(v);
+    else return v;
+}
+template <int GW>
+__device__ __forceinline__ double gsum(double v) {
+    if constexpr (GW == 64) return wave_sum(v);
+    else return row_sum(v);
+}
+template <int GW>
+__device__ __forceinline__ double gmax(double v) {
+    if constexpr (GW == 64) return wave_max(v);
+    else return row_max(v);
+}
+// value of v in lane k of the group (k uniform per group)
+template <int GW>
+__device__ __forceinline__ double gbcast(double v, int k) {
+    if constexpr (GW == 64) return bcast(v, k);
+    else return lane_pull(v, (int)(threadIdx.x & 48) + k);
+}
 
 #ifndef BR_CTL_INLINE
 #define BR_CTL_INLINE __forceinline__
@@ -208,7 +244,7 @@ enum { PH_F0 = 0, PH_HIN = 1, PH_NEWTON = 2, PH_EF1 = 3 };
 enum { A_RHS = 0, A_SOLVE = 1, A_SETUP = 2, A_DONE = 3 };
 
 // wrms norm of the lane's component values (components lane + 64 s) with weights ewt
-template <int CPL>
+template <int CPL, int GW = 64>
 __device__ __forceinline__ double wrms_l(const double (&v)[CPL], const double (&ewt)[CPL], int lane, int n) {
     double acc = 0.0;
 #pragma unroll
@@ -216,7 +252,7 @@ __device__ __forceinline__ double wrms_l(const double (&v)[CPL], const double (&
         const double t = (lane + 64 * s < n) ? v[s] * ewt[s] : 0.0;
         acc += t * t;
     }
-    return uni(sqrt(wave_sum(acc) / n));
+    return guni<GW>(sqrt(gsum<GW>(acc) / n));
 }
 // per-component slot loops over the lane's components c = lane + 64 s
 #define FOR_S for (int s = 0; s < CPL; ++s)
@@ -240,32 +276,33 @@ __device__ __forceinline__ P ld_ptr(const __attribute__((address_space(3))) P& f
     const unsigned lo = (unsigned)uni((int)(tv & 0xffffffffull)), hi = (unsigned)uni((int)(tv >> 32));
     return reinterpret_cast<P>(((unsigned long long)hi << 32) | lo);
 }
+template <int GW = 64>
 __device__ __forceinline__ CtlArgs load_args(LCtl* C) {
     CtlArgs a;
     a.rtol = ud(C->a_rtol); a.atol = ud(C->a_atol); a.hmax_inv = ud(C->a_hmax_inv); a.ufac = ud(C->a_ufac);
     a.trace = launder(ld_ptr(C->a_trace));
     a.tout = launder(ld_ptr(C->a_tout));
     a.yout = launder(ld_ptr(C->a_yout));
-    a.max_steps = ui(C->a_max_steps); a.trace_cap = ui(C->a_trace_cap); a.rid = ui(C->a_rid); a.n = ui(C->a_n);
-    a.ign = ui(C->a_ign); a.nout = ui(C->a_nout);
+    a.max_steps = gui<GW>(C->a_max_steps); a.trace_cap = gui<GW>(C->a_trace_cap); a.rid = gui<GW>(C->a_rid); a.n = gui<GW>(C->a_n);
+    a.ign = gui<GW>(C->a_ign); a.nout = gui<GW>(C->a_nout);
     return a;
 }
 
 // mole fraction of gas species k in state v (components lane + 64 s): (v_k/M_k) / sum_j v_j/M_j
-template <int CPL>
+template <int CPL, int GW = 64>
 __device__ __forceinline__ double mole_frac_of(const double (&v)[CPL], int lane, int k) {
     const double* mw = reinterpret_cast<const double*>(br_lds);   // staged molwt[] (image offset 0)
     const int ng = MF(ng);
     double g = 0.0, c0 = 0.0, c1 = 0.0;
 #pragma unroll
     FOR_S if (CS < ng) { const double c = v[s] / mw[CS]; g += c; if (s == 0) c0 = c; else c1 = c; }
-    const double ck = (k < 64) ? bcast(c0, k) : bcast(c1, k - 64);   // k uniform: one readlane pair
-    return ck / wave_sum(g);
+    const double ck = (k < 64) ? gbcast<GW>(c0, k) : gbcast<GW>(c1, k - 64);   // k uniform: one readlane pair
+    return ck / gsum<GW>(g);
 }
 // ignition marker after an accepted step to (tn, v): midpoint of the step with the largest dX/dt
-template <int CPL>
+template <int CPL, int GW = 64>
 __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int lane, double tn, const double (&v)[CPL]) {
-    const double x = uni(mole_frac_of<CPL>(v, lane, a.ign));
+    const double x = guni<GW>(mole_frac_of<CPL, GW>(v, lane, a.ign));
     const double t0 = ud(C->ign_t), xp = ud(C->ign_x), rate = ud(C->ign_rate);
     const double dt = tn - t0;   // > 0 (accepted step): compare without the division, divide on a new max
     if (x - xp > rate * dt) {
@@ -276,12 +313,12 @@ __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int la
 }
 // dense output (CVode CV_NORMAL): every tout in (t_{n-1}, t_n] from the Nordsieck array of the step
 // just completed, y(t) = sum_j z_j ((t - tn)/h)^j (CVodeGetDky, k = 0)
-template <int CPL>
-__device__ __forceinline__ void dense_output(LCtl* C, VT<CPL>& V, const CtlArgs& a, int lane, double tn, double h, int q,
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void dense_output(LCtl* C, VT<CPL, GW>& V, const CtlArgs& a, int lane, double tn, double h, int q,
                                              double tlim) {
-    int io = ui(C->iout);
+    int io = gui<GW>(C->iout);
     while (io < a.nout) {
-        const double t = uni(a.tout[io]);
+        const double t = guni<GW>(a.tout[io]);
         if (!(t <= tlim)) break;
         const double sk = (t - tn) / h;
         auto row = a.yout + ((size_t)a.rid * a.nout + io) * a.n;
@@ -309,15 +346,17 @@ struct AttemptIn {
     double h, tn, tstop, gammap;
     double tau[QMAX + 2];
 };
+template <int GW = 64>
 __device__ __forceinline__ AttemptIn load_attempt(LCtl* C) {
     AttemptIn in;
-    in.q = ui(C->q); in.qwait = ui(C->qwait); in.nst = ui(C->nst); in.nstlp = ui(C->nstlp);
+    in.q = gui<GW>(C->q); in.qwait = gui<GW>(C->qwait); in.nst = gui<GW>(C->nst); in.nstlp = gui<GW>(C->nstlp);
     in.h = ud(C->h); in.tn = ud(C->tn); in.tstop = ud(C->tstop); in.gammap = ud(C->gammap);
 #pragma unroll
     for (int i = 0; i < QMAX + 2; ++i) in.tau[i] = ud(C->tau[i]);
     return in;
 }
 // cvSet (BDF coefficients l[], tq[], gamma) for the current q, h, tau
+template <int GW = 64>
 __device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4_out, double& gamrat_out) {
     const int q = in.q, qwait = in.qwait, nst = in.nst;
     const double h = in.h;
@@ -403,9 +442,9 @@ __device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4
 }
 
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
-template <int CPL>
-__device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
-    const int q = ui(C->q);
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL, GW>& V, int lane) {
+    const int q = gui<GW>(C->q);
     const double eta = ud(C->eta), hscale = ud(C->hscale);
     double f = eta;
 #pragma unroll
@@ -420,8 +459,8 @@ __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL>& V, int lane) {
     C->h = h; C->hscale = h;
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
-template <int CPL>
-__device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane, const AttemptIn& in) {
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL, GW>& V, int lane, const AttemptIn& in) {
     const int q = in.q;
     double tn = in.tn + in.h;
     const double tstop = in.tstop;
@@ -441,9 +480,9 @@ __device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL>& V, int lane, const 
         for (int j = 0; j < QMAX; ++j) V.at(j, s) = z[j];
     }
 }
-template <int CPL>
-__device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL>& V, int lane) {
-    const int q = ui(C->q);
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL, GW>& V, int lane) {
+    const int q = gui<GW>(C->q);
     C->tn = ud(C->saved_t);
 #pragma unroll
     FOR_S {
@@ -460,9 +499,9 @@ __device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL>& V, int lane) {
     }
 }
 // cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
-template <int CPL>
-__device__ __forceinline__ void cv_adjust_order(LCtl* C, VT<CPL>& V, int lane, int dq) {
-    const int q = ui(C->q);
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void cv_adjust_order(LCtl* C, VT<CPL, GW>& V, int lane, int dq) {
+    const int q = gui<GW>(C->q);
     if (q == 2 && dq != 1) return;
     double lv[QMAX + 1] = {0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
     const double hscale = ud(C->hscale);
@@ -504,23 +543,23 @@ __device__ __forceinline__ void cv_adjust_order(LCtl* C, VT<CPL>& V, int lane, i
 }
 // trace row of an accepted step (save_data, src/BatchReactor.jl:383-402): t, h, q, the pressure
 // of the last RHS evaluation, the accepted state u_n, the state y of the last RHS evaluation
-template <int CPL>
+template <int CPL, int GW = 64>
 __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, int step, double t,
                                           const double (&v)[CPL], const double (&y)[CPL]) {
     if (a.trace && step <= a.trace_cap) {
         auto row = a.trace + ((size_t)a.rid * (a.trace_cap + 1) + step) * (2 * a.n + 4);
-        if (lane == 0) { row[0] = t; row[1] = ud(C->h); row[2] = (double)ui(C->q); row[3] = ud(C->p_last); }
+        if (lane == 0) { row[0] = t; row[1] = ud(C->h); row[2] = (double)gui<GW>(C->q); row[3] = ud(C->p_last); }
 #pragma unroll
         FOR_S if (CS < a.n) { row[4 + CS] = v[s]; row[4 + a.n + CS] = y[s]; }
     }
 }
 // one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
-template <int CPL>
-__device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int nflag) {
-    const AttemptIn in = load_attempt(C);
-    cv_predict<CPL>(C, V, lane, in);
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL, GW>& V, int lane, int nflag) {
+    const AttemptIn in = load_attempt<GW>(C);
+    cv_predict<CPL, GW>(C, V, lane, in);
     double tq4, gamrat;
-    cv_set(C, in, tq4, gamrat);
+    cv_set<GW>(C, in, tq4, gamrat);
     const int nst = in.nst;
     C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
     C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
@@ -534,11 +573,11 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL>& V, int lane, int
 #pragma unroll
     FOR_S V.at(V_Y, s) = V.at(0, s);   // y = z0
 }
-template <int CPL>
-__device__ __forceinline__ void begin_step(LCtl* C, VT<CPL>& V, int lane, const CtlArgs& a) {
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void begin_step(LCtl* C, VT<CPL, GW>& V, int lane, const CtlArgs& a) {
     BR_SUB_T(bt0);
     const double tn = ud(C->tn), hprime = ud(C->hprime), h = ud(C->h);   // read before the V stores
-    const int nst = ui(C->nst), qp = ui(C->qprime), q = ui(C->q);
+    const int nst = gui<GW>(C->nst), qp = gui<GW>(C->qprime), q = gui<GW>(C->q);
 #pragma unroll
     FOR_S {
         const double z0 = V.at(0, s);
@@ -548,24 +587,24 @@ __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL>& V, int lane, const 
     C->ncf = 0; C->nef = 0;
     if ((nst > 0) && (hprime != h)) {
         if (qp != q) {
-            cv_adjust_order<CPL>(C, V, lane, qp - q);
+            cv_adjust_order<CPL, GW>(C, V, lane, qp - q);
             C->q = qp; C->L = qp + 1; C->qwait = qp + 1;
         }
-        cv_rescale<CPL>(C, V, lane);
+        cv_rescale<CPL, GW>(C, V, lane);
     }
-    begin_attempt<CPL>(C, V, lane, FIRST_CALL);
+    begin_attempt<CPL, GW>(C, V, lane, FIRST_CALL);
     BR_SUB_ADD(7, bt0);
 }
 
 // Controller, part 1: after the RHS value f = F(y) of this lane is known.
 // Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
-template <int CPL>
-__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
-    const CtlArgs a = load_args(C);
+template <int CPL, int GW = 64>
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL, GW>& V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
+    const CtlArgs a = load_args<GW>(C);
     const int n = a.n;
-    C->nfe = ui(C->nfe) + 1;
-    const int phase = ui(C->phase);
+    C->nfe = gui<GW>(C->nfe) + 1;
+    const int phase = gui<GW>(C->phase);
     double z0[CPL];
 #pragma unroll
     FOR_S z0[s] = V.at(0, s);
@@ -577,15 +616,15 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const d
             const double delta = (rl1 * V.at(1, s) + acor) - gamma * f[s];   // cvNlsResidual
             rhs_out[s] = -delta;
         }
-        if (ui(C->m_it) == 0 && ui(C->callSetup)) {          // cvLsSetup decision
-            const int nst = ui(C->nst);
+        if (gui<GW>(C->m_it) == 0 && gui<GW>(C->callSetup)) {          // cvLsSetup decision
+            const int nst = gui<GW>(C->nst);
             const double dgamma = fabs(ud(C->gamma) / ud(C->gammap) - 1.0);
-            const int cf = ui(C->jbad) ? FAIL_BAD_J : ui(C->convfail);
-            const int newj = (nst == 0) || (nst > ui(C->nstlj) + LS_MSBJ) || ((cf == FAIL_BAD_J) && (dgamma < LS_DGMAX)) ||
+            const int cf = gui<GW>(C->jbad) ? FAIL_BAD_J : gui<GW>(C->convfail);
+            const int newj = (nst == 0) || (nst > gui<GW>(C->nstlj) + LS_MSBJ) || ((cf == FAIL_BAD_J) && (dgamma < LS_DGMAX)) ||
                              (cf == FAIL_OTHER);
             C->newj = newj;
-            if (newj) { C->nje = ui(C->nje) + 1; C->nstlj = nst; }
-            C->nsetups = ui(C->nsetups) + 1;
+            if (newj) { C->nje = gui<GW>(C->nje) + 1; C->nstlj = nst; }
+            C->nsetups = gui<GW>(C->nsetups) + 1;
             C->jcur_nls = newj;
             C->gamrat = 1.0; C->gammap = ud(C->gamma); C->crate = 1.0; C->nstlp = nst;
             return A_SETUP;
@@ -597,7 +636,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const d
         const double hh = ud(C->h);
 #pragma unroll
         FOR_S V.at(1, s) = hh * f[s];
-        begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
+        begin_attempt<CPL, GW>(C, V, lane, PREV_ERR_FAIL);
         C->phase = PH_NEWTON;
         return A_RHS;
     }
@@ -618,7 +657,7 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const d
             V.at(1, s) = f[s];
             if (CS < n) ratio = fmax(ratio, fabs(f[s]) / (HUB_FACTOR * fabs(z0[s]) + 1.0 / ewt[s]));
         }
-        const double hub_inv = uni(wave_max(ratio));
+        const double hub_inv = guni<GW>(gmax<GW>(ratio));
         double hub = HUB_FACTOR * tdist;
         if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
         const double hg = sqrt(hlb * hub);
@@ -638,10 +677,10 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const d
         double tempv[CPL];
 #pragma unroll
         FOR_S tempv[s] = (f[s] - z1in[s]) * (1.0 / hg);
-        const double yddnrm = wrms_l<CPL>(tempv, ewt, lane, n);
-        const int count1 = ui(C->count1);
+        const double yddnrm = wrms_l<CPL, GW>(tempv, ewt, lane, n);
+        const int count1 = gui<GW>(C->count1);
         double hnew;
-        if (ui(C->hnewOK) || count1 == MAX_ITERS) {
+        if (gui<GW>(C->hnewOK) || count1 == MAX_ITERS) {
             hnew = hg;
         } else {
             hnew = (yddnrm * hub * hub > 2.0) ? sqrt(2.0 / yddnrm) : sqrt(hg * hub);
@@ -667,11 +706,11 @@ __device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL>& V, int lane, const d
     const double tn = ud(C->tn), tstop = ud(C->tstop);
     if ((tn + h - tstop) * h > 0.0) h = (tstop - tn) * (1.0 - 4.0 * UROUND);
     C->h = h; C->hscale = h; C->hprime = h;
-    trace_row<CPL>(C, a, lane, 0, 0.0, z0, z0);
+    trace_row<CPL, GW>(C, a, lane, 0, 0.0, z0, z0);
 #pragma unroll
     FOR_S V.at(1, s) *= h;
     if (a.max_steps <= 0) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
-    begin_step<CPL>(C, V, lane, a);
+    begin_step<CPL, GW>(C, V, lane, a);
     C->phase = PH_NEWTON;
     return A_RHS;
 }
@@ -702,10 +741,10 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 // Controller, part 2: after the linear solve (delta = this lane's Newton correction) or after
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
-template <int CPL>
-__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, double (&delta)[CPL], int lu_fail) {
+template <int CPL, int GW = 64>
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, double (&delta)[CPL], int lu_fail) {
     BR_SUB_T(ps0);
-    const CtlArgs a = load_args(C);
+    const CtlArgs a = load_args<GW>(C);
     const int n = a.n;
     double ewt[CPL], acor[CPL];
 #pragma unroll
@@ -716,9 +755,9 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     if (lu_fail) {
         nls = 2;
     } else {
-        C->nni = ui(C->nni) + 1;
+        C->nni = gui<GW>(C->nni) + 1;
         const double gamrat = ud(C->gamrat);
-        const int m = ui(C->m_it);                            // read before the V stores
+        const int m = gui<GW>(C->m_it);                            // read before the V stores
         double crate = ud(C->crate);
         const double delp = ud(C->delp), tol = ud(C->tol);
 #pragma unroll
@@ -727,11 +766,11 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
             acor[s] = V.at(V_ACOR, s) + delta[s];
             V.at(V_ACOR, s) = acor[s];
         }
-        const double del = wrms_l<CPL>(delta, ewt, lane, n);     // cvNlsConvTest
+        const double del = wrms_l<CPL, GW>(delta, ewt, lane, n);     // cvNlsConvTest
         if (m > 0) { crate = fmax(CRDOWN * crate, del / delp); C->crate = crate; }
         const double dcon = del * fmin(1.0, crate) / tol;
         if (dcon <= 1.0) {
-            acnrm = (m == 0) ? del : wrms_l<CPL>(acor, ewt, lane, n);
+            acnrm = (m == 0) ? del : wrms_l<CPL, GW>(acor, ewt, lane, n);
             C->acnrm = acnrm;
             nls = 0;
         } else {
@@ -746,7 +785,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
                 FOR_S V.at(V_Y, s) = V.at(0, s) + acor[s];
                 return A_RHS;
             }
-            if (!ui(C->jcur_nls)) {                          // retry with a fresh Jacobian
+            if (!gui<GW>(C->jcur_nls)) {                          // retry with a fresh Jacobian
                 C->callSetup = 1; C->jbad = 1; C->m_it = 0;
 #pragma unroll
                 FOR_S {
@@ -759,41 +798,41 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
         }
     }
     if (nls != 0) {                                          // cvHandleNFlag
-        C->ncfn = ui(C->ncfn) + 1;
-        cv_restore<CPL>(C, V, lane);
-        const int ncf = ui(C->ncf) + 1;
+        C->ncfn = gui<GW>(C->ncfn) + 1;
+        cv_restore<CPL, GW>(C, V, lane);
+        const int ncf = gui<GW>(C->ncf) + 1;
         C->ncf = ncf;
         C->etamax = 1.0;
         if (ncf == MXNCF) { C->status = BR_ERR_CONV; return A_DONE; }
         C->eta = ETACF;
-        cv_rescale<CPL>(C, V, lane);
-        begin_attempt<CPL>(C, V, lane, PREV_CONV_FAIL);
+        cv_rescale<CPL, GW>(C, V, lane);
+        begin_attempt<CPL, GW>(C, V, lane, PREV_CONV_FAIL);
         return A_RHS;
     }
     // ---- cvDoErrorTest
     const double dsm = acnrm * tq2_e;
-    const int q = ui(C->q);
+    const int q = gui<GW>(C->q);
     if (dsm > 1.0) {
-        const int nef = ui(C->nef) + 1;
-        C->nef = nef; C->netf = ui(C->netf) + 1;
-        cv_restore<CPL>(C, V, lane);
+        const int nef = gui<GW>(C->nef) + 1;
+        C->nef = nef; C->netf = gui<GW>(C->netf) + 1;
+        cv_restore<CPL, GW>(C, V, lane);
         if (nef == MXNEF) { C->status = BR_ERR_ERRTEST; return A_DONE; }
         C->etamax = 1.0;
         if (nef <= MXNEF1) {
-            double eta = 1.0 / (root_int(BIAS2 * dsm, ui(C->L)) + ADDON);
+            double eta = 1.0 / (root_int(BIAS2 * dsm, gui<GW>(C->L)) + ADDON);
             eta = fmax(ETAMIN, eta);
             if (nef >= SMALL_NEF) eta = fmin(eta, ETAMXF);
             C->eta = eta;
-            cv_rescale<CPL>(C, V, lane);
-            begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
+            cv_rescale<CPL, GW>(C, V, lane);
+            begin_attempt<CPL, GW>(C, V, lane, PREV_ERR_FAIL);
             return A_RHS;
         }
         if (q > 1) {
             C->eta = ETAMIN;
-            cv_adjust_order<CPL>(C, V, lane, -1);
+            cv_adjust_order<CPL, GW>(C, V, lane, -1);
             C->L = q; C->q = q - 1; C->qwait = q;
-            cv_rescale<CPL>(C, V, lane);
-            begin_attempt<CPL>(C, V, lane, PREV_ERR_FAIL);
+            cv_rescale<CPL, GW>(C, V, lane);
+            begin_attempt<CPL, GW>(C, V, lane, PREV_ERR_FAIL);
             return A_RHS;
         }
         C->eta = ETAMIN;
@@ -810,19 +849,19 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     // every controller scalar this part reads, loaded in one batch before the first Nordsieck store
     // (V shares LDS with the controller, so a load placed after a V store cannot be hoisted above
     // it: read in place, each one was its own LDS round trip)
-    const int nst = ui(C->nst) + 1;
+    const int nst = gui<GW>(C->nst) + 1;
     const double h = ud(C->h);
     double tauv[QMAX + 1], lv[QMAX + 1];
 #pragma unroll
     for (int i = 1; i <= QMAX; ++i) tauv[i] = ud(C->tau[i]);
 #pragma unroll
     for (int j = 0; j <= QMAX; ++j) lv[j] = ud(C->l[j]);
-    int qwait = ui(C->qwait) - 1;
+    int qwait = gui<GW>(C->qwait) - 1;
     const double etamax = ud(C->etamax), tq1 = ud(C->tq[1]), tq2 = ud(C->tq[2]), tq3 = ud(C->tq[3]);
     const double tq5 = ud(C->tq[5]);
     double saved_tq5 = ud(C->saved_tq5);
-    const int L = ui(C->L);
-    const int nstloc = ui(C->nstloc) + 1;
+    const int L = gui<GW>(C->L);
+    const int nstloc = gui<GW>(C->nstloc) + 1;
     const double tn = ud(C->tn), tstop = ud(C->tstop), ulimit = ud(C->ulimit);
     C->nst = nst;
     double tau2 = tauv[2];   // tau[2] after the shift
@@ -861,7 +900,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
                 double zq[CPL];
 #pragma unroll
                 FOR_S zq[s] = vget<CPL>(V, q, s);
-                const double ddn = wrms_l<CPL>(zq, ewt, lane, n) * tq1;
+                const double ddn = wrms_l<CPL, GW>(zq, ewt, lane, n) * tq1;
                 etaqm1 = 1.0 / (root_int(BIAS1 * ddn, q) + ADDON);
             }
             if (q != QMAX && saved_tq5 != 0.0) {
@@ -869,7 +908,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
                 double tempv[CPL];
 #pragma unroll
                 FOR_S tempv[s] = acor[s] - cquot * V.at(QMAX, s);
-                const double dup = wrms_l<CPL>(tempv, ewt, lane, n) * tq3;
+                const double dup = wrms_l<CPL, GW>(tempv, ewt, lane, n) * tq3;
                 etaqp1 = 1.0 / (root_int(BIAS3 * dup, L + 1) + ADDON);
             }
             const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
@@ -905,21 +944,21 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
         double zm = 0.0;
 #pragma unroll
         FOR_S if (CS < n) { const double a = fabs(z0[s]); zm = fmax(zm, a == a ? a : INFINITY); }
-        const double mx = uni(wave_max(zm));
+        const double mx = guni<GW>(gmax<GW>(zm));
         if (!(mx < INFINITY) || mx > ulimit) { C->status = BR_ERR_UNSTABLE; return A_DONE; }
     }
     if (a.trace) {
         double yl[CPL];
 #pragma unroll
         FOR_S yl[s] = V.at(V_Y, s);                     // the last RHS was evaluated at y
-        trace_row<CPL>(C, a, lane, nst, tn, z0, yl);
+        trace_row<CPL, GW>(C, a, lane, nst, tn, z0, yl);
     }
-    if (a.ign >= 0) track_ignition<CPL>(C, a, lane, tn, z0);
-    if (a.nout) dense_output<CPL>(C, V, a, lane, tn, h, q, tn);
+    if (a.ign >= 0) track_ignition<CPL, GW>(C, a, lane, tn, z0);
+    if (a.nout) dense_output<CPL, GW>(C, V, a, lane, tn, h, q, tn);
     // CVode ONE_STEP + tstop handling
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
     if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
-        if (a.nout) dense_output<CPL>(C, V, a, lane, tn, h, q, tstop);
+        if (a.nout) dense_output<CPL, GW>(C, V, a, lane, tn, h, q, tstop);
         const double sk = (tstop - tn) / h;
 #pragma unroll
         FOR_S {
@@ -942,7 +981,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
     }
     if (nstloc >= a.max_steps) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
     BR_SUB_ADD(10, ps2);
-    begin_step<CPL>(C, V, lane, a);
+    begin_step<CPL, GW>(C, V, lane, a);
     return A_RHS;
 }
 
@@ -953,32 +992,32 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL>& V, int lane, doubl
 // kernel's single RHS call site (k_integrate: the column index `dqj` routes the result here).
 constexpr double DQ_SRUR = 1.4901161193847656e-08;   // sqrt(UROUND) = 2^-26
 constexpr double DQ_MIN_INC_MULT = 1000.0;
-template <int CPL>
-__device__ __forceinline__ void dq_begin(LCtl* C, VT<CPL>& V, int lane, const double (&f)[CPL]) {
-    const int n = ui(C->a_n);
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void dq_begin(LCtl* C, VT<CPL, GW>& V, int lane, const double (&f)[CPL]) {
+    const int n = gui<GW>(C->a_n);
     double ewt[CPL];
 #pragma unroll
     FOR_S {
         ewt[s] = V.at(V_EWT, s);
         V.at(V_TEMP, s) = f[s];                      // fy, kept for the n columns
     }
-    const double fnorm = wrms_l<CPL>(f, ewt, lane, n);
+    const double fnorm = wrms_l<CPL, GW>(f, ewt, lane, n);
     C->dq_mininc = (fnorm != 0.0) ? (DQ_MIN_INC_MULT * fabs(ud(C->h)) * UROUND * n * fnorm) : 1.0;
 }
 // increment of this lane's components (the one for component j is used by column j)
-template <int CPL>
-__device__ __forceinline__ void dq_incs(LCtl* C, VT<CPL>& V, int lane, double (&inc)[CPL]) {
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void dq_incs(LCtl* C, VT<CPL, GW>& V, int lane, double (&inc)[CPL]) {
     const double mininc = ud(C->dq_mininc);
 #pragma unroll
     FOR_S inc[s] = fmax(DQ_SRUR * fabs(V.at(V_Z0, s)), mininc / V.at(V_EWT, s));
 }
 // column j of the saved J from F(y + inc_j e_j) = f (rows as jacobian(): JW per column)
-template <int CPL>
-__device__ __forceinline__ void dq_column(LCtl* C, VT<CPL>& V, int lane, int j, const double (&f)[CPL], double* Jsave) {
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void dq_column(LCtl* C, VT<CPL, GW>& V, int lane, int j, const double (&f)[CPL], double* Jsave) {
     constexpr int JW = CPL == 2 ? 80 : 64;
     double inc[CPL];
-    dq_incs<CPL>(C, V, lane, inc);
-    const double ij = (j < 64) ? bcast(inc[0], j) : bcast(inc[CPL - 1], j - 64);
+    dq_incs<CPL, GW>(C, V, lane, inc);
+    const double ij = (j < 64) ? gbcast<GW>(inc[0], j) : gbcast<GW>(inc[CPL - 1], j - 64);
     const double ii = 1.0 / ij;
     BR_GLOBAL double* col = launder(Jsave) + (size_t)j * JW;
 #pragma unroll
@@ -987,11 +1026,11 @@ __device__ __forceinline__ void dq_column(LCtl* C, VT<CPL>& V, int lane, int j, 
         if (s == 0) col[lane] = v;
         else if (lane < 16) col[64 + lane] = v;
     }
-    C->nfe_dq = ui(C->nfe_dq) + 1;
+    C->nfe_dq = gui<GW>(C->nfe_dq) + 1;
 }
 // the Newton right-hand side at the setup point again (cvNlsResidual with f = fy, as ctl_post_rhs)
-template <int CPL>
-__device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL>& V, int lane, double (&b)[CPL]) {
+template <int CPL, int GW = 64>
+__device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane, double (&b)[CPL]) {
     const double rl1 = ud(C->rl1), gamma = ud(C->gamma);
 #pragma unroll
     FOR_S b[s] = -((rl1 * V.at(1, s) + V.at(V_ACOR, s)) - gamma * V.at(V_TEMP, s));

@@ -234,6 +234,23 @@ __device__ __forceinline__ double wave_max(double v) {
     return bcast(v, 63);
 }
 
+// sum / max over each 16-lane DPP row (the quad engine's reactor groups): the butterfly steps of
+// wave_sum / wave_max without the cross-row ones; every lane of a row gets its row's value
+__device__ __forceinline__ double row_sum(double v) {
+    v += dppd<0xB1>(v);
+    v += dppd<0x4E>(v);
+    v += dppd<0x141>(v);
+    v += dppd<0x140>(v);
+    return v;
+}
+__device__ __forceinline__ double row_max(double v) {
+    v = fmax(v, dppd<0xB1>(v));
+    v = fmax(v, dppd<0x4E>(v));
+    v = fmax(v, dppd<0x141>(v));
+    v = fmax(v, dppd<0x140>(v));
+    return v;
+}
+
 // opaque copy of a uniform pointer: addresses derived from it cannot be hoisted out of the
 // integrator's main loop (otherwise LICM keeps ~NMAX 64-bit column addresses live across the
 // whole loop and the kernel spills)
