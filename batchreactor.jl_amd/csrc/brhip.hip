@@ -1037,6 +1037,7 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane,
 }
 
 #include "brhip_lane.hpp"   // one reactor per lane (small gas mechanisms)
+#include "brhip_quad.hpp"   // four reactors per wave, one per 16-lane DPP row (small gas mechanisms)
 
 // ------------------------------------------------------------------------------------
 // the integrator kernel: one reactor per 64-lane wavefront, `rpb` reactors per workgroup
@@ -1424,6 +1425,11 @@ struct br_mech {
     double* lws = nullptr;     // saved Jacobians, slot-major [NM*NM][slots]
     size_t lws_bytes = 0;
     int* queue = nullptr;      // work counter
+    // four-reactors-per-wave engine (brhip_quad.hpp): 0 = not eligible, else the register width NM
+    int quad_nm = 0, quad_blocks = 0;
+    size_t quad_shmem = 0;
+    double* qws = nullptr;     // saved Jacobians, 16 x 16 per group slot
+    size_t qws_bytes = 0;
     int* wq = nullptr;         // k_integrate work counter
     double* defer_t0 = nullptr; // start time of each deferred lane reactor (DEFER_CAP)
     int ncu = 0;
@@ -1470,10 +1476,23 @@ int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs) {
     return 0;
 }
 
+// engine selection for br_integrate* (untraced): BRHIP_ENGINE = wave | lane | quad forces one (when
+// the mechanism is eligible); default: the quad engine for eligible mechanisms with the analytic
+// Jacobian when BR_QUAD_DEFAULT, else the lane engine, else the wavefront engine
+#ifndef BR_QUAD_DEFAULT
+#define BR_QUAD_DEFAULT 0
+#endif
+static int pick_engine(const br_mech* m, bool dq_jac) {
+    const char* eng = getenv("BRHIP_ENGINE");
+    if (eng && strcmp(eng, "wave") == 0) return 0;
+    if (eng && strcmp(eng, "lane") == 0) return m->lane_nm;
+    const bool want_quad = (eng && strcmp(eng, "quad") == 0) || BR_QUAD_DEFAULT;
+    if (m->quad_nm && !dq_jac && want_quad) return -m->quad_nm;
+    return m->lane_nm;
+}
 int br_mech_engine(const br_mech* m) {
     if (!m) return fail(BR_ERR_INPUT, "null mechanism");
-    const char* eng = getenv("BRHIP_ENGINE");
-    return (eng && strcmp(eng, "wave") == 0) ? 0 : m->lane_nm;
+    return pick_engine(m, false);
 }
 
 int br_mech_launch_info(const br_mech* m, int* rpb, int* waves_per_cu, long long* lds_bytes) {
@@ -1831,6 +1850,21 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
             m->lane_blocks = nb * ncu;
         }
     }
+    // ---- four reactors per wave for small gas-only mechanisms (brhip_quad.hpp)
+    if (ns == 0 && n <= 16 && M.nset <= quad::MAX_SETS) {
+        m->quad_nm = n <= 9 ? 9 : 16;
+        const void* qfn = m->quad_nm == 9 ? (const void*)k_quad<9> : (const void*)k_quad<16>;
+        m->quad_shmem = (size_t)M.img_bytes + (size_t)BR_QWPB * 4 * quad::block_bytes(nrg, M.nfo);
+        int nb = 0;
+        if (m->quad_shmem > LDS_PER_CU ||
+            hipFuncSetAttribute(qfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->quad_shmem) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, qfn, 64 * BR_QWPB, m->quad_shmem) != hipSuccess || nb <= 0) {
+            m->quad_nm = 0;
+        } else {
+            nb = std::min(nb, (int)(LDS_PER_CU / ((m->quad_shmem + LDS_GRANULE - 1) / LDS_GRANULE * LDS_GRANULE)));
+            m->quad_blocks = nb * m->ncu;
+        }
+    }
     HIPCHK(hipEventCreate(&m->ev0));
     HIPCHK(hipEventCreate(&m->ev1));
     *out = m;
@@ -1844,6 +1878,7 @@ int br_mech_destroy(br_mech* m) {
     if (m->ws) hipFree(m->ws);
     if (m->jws) hipFree(m->jws);
     if (m->lws) hipFree(m->lws);
+    if (m->qws) hipFree(m->qws);
     if (m->queue) hipFree(m->queue);
     if (m->wq) hipFree(m->wq);
     if (m->defer_t0) hipFree(m->defer_t0);
@@ -1987,8 +2022,37 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.rid_t0 = nullptr;
     o.work = nullptr;
     hipStream_t s = (hipStream_t)stream;
-    const char* eng = getenv("BRHIP_ENGINE");   // "wave" forces the wave-per-reactor engine
-    if (m->lane_nm && !trace && !(eng && strcmp(eng, "wave") == 0)) {
+    const int engine = trace ? 0 : pick_engine(m, o.dq_jac != 0);   // traced runs: the wavefront engine
+    if (engine < 0) {
+        // four reactors per wave (one per 16-lane row), persistent grid over the resident
+        // workgroups, reactors from a work counter
+        const int NM = -engine;
+        const int gpb = BR_QWPB * 4;
+        const int blocks = std::max(1, std::min((N + gpb - 1) / gpb, m->quad_blocks));
+        const size_t need = (size_t)blocks * gpb * quad::G * quad::G * sizeof(double);
+        if (m->qws_bytes < need) {
+            if (m->qws) hipFree(m->qws);
+            m->qws = nullptr; m->qws_bytes = 0;
+            HIPCHK(hipMalloc((void**)&m->qws, need));
+            m->qws_bytes = need;
+        }
+        if (!m->queue) HIPCHK(hipMalloc((void**)&m->queue, (2 + DEFER_CAP) * sizeof(int)));
+        HIPCHK(hipMemsetAsync(m->queue, 0, 2 * sizeof(int), s));
+        o.work = m->queue;
+        HIPCHK(hipEventRecord(m->ev0, s));
+        if (NM == 9) {
+            HIPCHK(hipFuncSetAttribute((const void*)k_quad<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->quad_shmem));
+            hipLaunchKernelGGL(k_quad<9>, dim3(blocks), dim3(64 * BR_QWPB), m->quad_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->qws);
+        } else {
+            HIPCHK(hipFuncSetAttribute((const void*)k_quad<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->quad_shmem));
+            hipLaunchKernelGGL(k_quad<16>, dim3(blocks), dim3(64 * BR_QWPB), m->quad_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->qws);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(m->ev1, s));
+        m->ev_recorded = true;
+        return 0;
+    }
+    if (engine > 0) {
         // one reactor per lane; reactors still running after defer_steps steps (a few per 1e4 on
         // H2/O2, some of them up to max_steps) are handed to a follow-up wavefront pass, whose
         // per-step latency for a lone reactor is far lower than a wave's with one live lane

@@ -61,12 +61,14 @@ class Engine:
     def kernel_name(self) -> str:
         """the integrator kernel br_integrate_dev launches for this mechanism"""
         nm = _lib.lib().br_mech_engine(self.h)
-        return f"k_lane<{nm}>" if nm > 0 else f"k_integrate<{self.nmax}>"
+        return f"k_lane<{nm}>" if nm > 0 else f"k_quad<{-nm}>" if nm < 0 else f"k_integrate<{self.nmax}>"
 
     @property
     def engine(self) -> str:
-        """'lane' (one reactor per lane, small gas mechanisms) or 'wave' (one reactor per wavefront)"""
-        return "lane" if _lib.lib().br_mech_engine(self.h) > 0 else "wave"
+        """'lane' (one reactor per lane), 'quad' (four reactors per wavefront, one per 16-lane row;
+        both for small gas mechanisms) or 'wave' (one reactor per wavefront)"""
+        nm = _lib.lib().br_mech_engine(self.h)
+        return "lane" if nm > 0 else "quad" if nm < 0 else "wave"
 
     @property
     def launch_info(self) -> dict:

@@ -657,6 +657,66 @@ def test_lane_and_wave_engines_agree(pkg, gpu, monkeypatch):
     assert max(close_states(Ul[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(96)) <= 1.0
 
 
+def test_quad_engine_h2o2(pkg, orc, gpu, monkeypatch):
+    """Four-reactors-per-wave engine (k_quad: one reactor per 16-lane DPP row, the wavefront
+    engine's CVODE controller instantiated for 16-lane groups, analytic Jacobian, LU in registers).
+    N = 200 with ragged end times: groups take new reactors from the work counter while the other
+    groups of their wave are mid-run. Tight tolerances: end states agree with the oracle to 1e-6
+    relative. Default tolerances with dense output: ignition time, the per-window bounds of
+    test_integrate_parity and the step counts as there."""
+    monkeypatch.setenv("BRHIP_ENGINE", "quad")
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    assert eng.engine == "quad" and eng.kernel_name == "k_quad<9>"
+    N = 200
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", N, 6)
+    tf = np.where(np.arange(N) % 3 == 0, 1e-3, 1e-2)            # ragged end times
+    U, st = eng.integrate(T, Asv, U0, tf, rtol=1e-10, atol=1e-16)
+    assert np.all(st["status"] == 0), np.unique(st["status"])
+    for i in range(N):
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], tf[i], analytic_jac=True, rtol=1e-10, atol=1e-16)
+        assert so["status"] == 0
+        assert close_states(U[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, i
+    from batchreactor_amd import ensemble
+    N = 128
+    T, Asv, U0 = ensemble.make_inputs(pm, "h2o2", 0, N)
+    U, st = eng.integrate(T, Asv, U0, 10.0, tout=OUT_T)
+    assert np.all(st["status"] == 0)
+    bounds = BOUNDS[("h2o2", False)]
+    nst_o = 0
+    for i in range(N):
+        uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], 10.0, OUT_T, analytic_jac=True)
+        ti = so["t_ign"]
+        assert abs(st["t_ign"][i] - ti) <= bounds[3] * max(st["ign_dt"][i], so["ign_dt"]) + 1e-4 * ti, i
+        eb = _band_errors(st["yout"][i], Yo, ti)
+        for w, (bound, e) in enumerate(zip(bounds[:3], eb)):
+            assert e <= bound, (i, ("pre", "front", "post")[w], e, bound)
+        assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.35 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
+        nst_o += so["nsteps"]
+    assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
+
+
+def test_quad_engine_step_budget_and_wave_agreement(pkg, orc, gpu, monkeypatch):
+    """k_quad: max_steps = 60 stops every reactor that needs more with BR_ERR_MAXSTEPS (-1) after
+    exactly 60 steps, as the oracle's CVODE run; and the quad and wavefront engines (same
+    controller, same analytic Jacobian) give the same end states at tight tolerances."""
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", 96, 12)
+    monkeypatch.setenv("BRHIP_ENGINE", "quad")
+    assert eng.engine == "quad"
+    U, st = eng.integrate(T[:64], Asv[:64], U0[:64], 10.0, max_steps=60)
+    for i in range(64):
+        _, so, _ = om.integrate(T[i], Asv[i], U0[i], 10.0, analytic_jac=True, max_steps=60)
+        assert so["status"] == -1 and so["nsteps"] == 60
+        assert st["status"][i] == -1 and st["nsteps"][i] == 60, (i, st["status"][i], st["nsteps"][i])
+    Uq, sq = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    monkeypatch.setenv("BRHIP_ENGINE", "wave")
+    Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    assert np.all(sq["status"] == 0) and np.all(sw["status"] == 0)
+    assert max(close_states(Uq[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(96)) <= 1.0
+
+
 def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
     """Reactors still running after BRHIP_DEFER_STEPS steps in the lane engine are handed to the
     wavefront engine, which continues them from their last accepted lane state (a CVODE restart at
