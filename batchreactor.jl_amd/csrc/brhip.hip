@@ -1477,22 +1477,22 @@ int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs) {
 }
 
 // engine selection for br_integrate* (untraced): BRHIP_ENGINE = wave | lane | quad forces one (when
-// the mechanism is eligible); default: the quad engine for eligible mechanisms with the analytic
-// Jacobian when BR_QUAD_DEFAULT, else the lane engine, else the wavefront engine
+// the mechanism is eligible); default: the quad engine for eligible mechanisms when BR_QUAD_DEFAULT,
+// else the lane engine, else the wavefront engine
 #ifndef BR_QUAD_DEFAULT
 #define BR_QUAD_DEFAULT 0
 #endif
-static int pick_engine(const br_mech* m, bool dq_jac) {
+static int pick_engine(const br_mech* m) {
     const char* eng = getenv("BRHIP_ENGINE");
     if (eng && strcmp(eng, "wave") == 0) return 0;
     if (eng && strcmp(eng, "lane") == 0) return m->lane_nm;
     const bool want_quad = (eng && strcmp(eng, "quad") == 0) || BR_QUAD_DEFAULT;
-    if (m->quad_nm && !dq_jac && want_quad) return -m->quad_nm;
+    if (m->quad_nm && want_quad) return -m->quad_nm;
     return m->lane_nm;
 }
 int br_mech_engine(const br_mech* m) {
     if (!m) return fail(BR_ERR_INPUT, "null mechanism");
-    return pick_engine(m, false);
+    return pick_engine(m);
 }
 
 int br_mech_launch_info(const br_mech* m, int* rpb, int* waves_per_cu, long long* lds_bytes) {
@@ -2022,7 +2022,7 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     o.rid_t0 = nullptr;
     o.work = nullptr;
     hipStream_t s = (hipStream_t)stream;
-    const int engine = trace ? 0 : pick_engine(m, o.dq_jac != 0);   // traced runs: the wavefront engine
+    const int engine = trace ? 0 : pick_engine(m);   // traced runs: the wavefront engine
     if (engine < 0) {
         // four reactors per wave (one per 16-lane row), persistent grid over the resident
         // workgroups, reactors from a work counter

@@ -250,8 +250,22 @@ __device__ __forceinline__ void q_jac(const Tab& tb, const double* sp, const dou
     for (int j = 0; j < NM; ++j) jr[j] = (gl < n && j < n) ? jr[j] * (Mk / tb.molwt[j]) : 0.0;
 }
 
-// group pivot: the first max |a| (bit patterns: a 32-bit max over the high words, then the low
-// words, then the lowest row) among candidate rows of the group; returns the lane within the group
+// compile-time loop: f(std::integral_constant<int, K>) for K = B .. E-1
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+// value of lane K of this lane's 16-lane row (DPP row_newbcast: a VALU move, no LDS crossbar)
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) { return dppd<0x150 + K>(v); }
+
+// group pivot of step k: the first max |a| (bit patterns: a 32-bit max over the high words, then
+// over the low words, then the lowest lane) among candidate lanes of the row; returns that lane
+// within the group. SUNDIALS denseGETRF takes the first row of largest |a_ik| in the current
+// (already interchanged) row order -- the lane order here.
 __device__ __forceinline__ int q_pivot(double a, bool cand, int gl) {
     const unsigned long long bits = (unsigned long long)__double_as_longlong(a) & 0x7fffffffffffffffull;
     const unsigned hi = cand ? (unsigned)(bits >> 32) : 0u;
@@ -264,79 +278,100 @@ __device__ __forceinline__ int q_pivot(double a, bool cand, int gl) {
     return (int)(~row_umax(key));
 }
 
-// LU of A = I - gamma J (rows in natural order, row gl per lane, SUNDIALS denseGETRF pivoting),
-// in registers: a[k] of row r holds the multiplier l_rk for the steps k before r was pivoted, the
-// U row from its own step on. pstep: the step that pivoted this row (1024: no row); pk[k]: the lane
-// (within the group) of step k's pivot row; dinv: 1 / pivot of this row. Returns 0 or k+1 (zero pivot).
+// LU of A = I - gamma J with partial pivoting as SUNDIALS denseGETRF (src/BatchReactor.jl:204-210:
+// CVODE's dense linear solver), one row per lane in registers, rows interchanged physically (lane
+// = current row position): after the factorization lane s holds row s of the factors (L's
+// multipliers in a[k < s], U in a[k >= s]), dinv = 1 / u_ss, and orig = the original row now at
+// lane s (the accumulated interchanges, applied to b by q_solve). Interchanges are bpermutes of the
+// two rows' registers, issued only when some group of the wave needs one; the pivot row's values
+// reach the row by DPP row broadcasts. Returns 0 or k+1 (zero pivot at step k, as denseGETRF).
 template <int NM>
-__device__ __forceinline__ int q_lu(const double (&jr)[NM], double gamma, int n, int gl, double (&a)[NM], int& pstep,
-                                    int (&pk)[NM], double& dinv) {
+__device__ __forceinline__ int q_lu(const double (&jr)[NM], double gamma, int n, int gl, double (&a)[NM], int& orig,
+                                    double& dinv) {
     const int gb = (int)(threadIdx.x & 48);
 #pragma unroll
     for (int j = 0; j < NM; ++j) a[j] = ((j == gl && gl < n) ? 1.0 : 0.0) - gamma * jr[j];
-    pstep = gl < n ? -1 : 1024;
+    orig = gl;
     dinv = 0.0;
     int fail = 0;
-#pragma unroll
-    for (int k = 0; k < NM; ++k) {
-        pk[k] = 0;
+    sfor<0, NM>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
         if (k < n) {
-            const bool cand = pstep < 0;
-            const int p = q_pivot(a[k], cand, gl);
-            pk[k] = p;
-            const double pv = lane_pull(a[k], gb + p);
+            const int p = q_pivot(a[k], gl >= k && gl < n, gl);
+            if (__ballot(p != k) != 0) {                           // interchange rows k and p
+                const int src = gb + (gl == k ? p : (gl == p ? k : gl));
+#pragma unroll
+                for (int j = 0; j < NM; ++j) a[j] = lane_pull(a[j], src);
+                orig = __builtin_amdgcn_ds_bpermute(src * 4, orig);
+            }
+            const double pv = row_bcast<k>(a[k]);
             if (pv == 0.0 && fail == 0) fail = k + 1;
             const double rinv = 1.0 / pv;
-            const bool isp = gl == p;
-            const bool rem = cand && !isp;
-            const double l = rem ? a[k] * rinv : 0.0;
-            if (rem) a[k] = l;
-            if (isp) { pstep = k; dinv = rinv; }
+            const bool below = gl > k;
+            const double l = below ? a[k] * rinv : 0.0;                // denseGETRF: a_ik *= 1 / a_kk
+            if (below) a[k] = l;
+            if (gl == k) dinv = rinv;
 #pragma unroll
             for (int j = k + 1; j < NM; ++j)
-                if (j < n) a[j] = fma(-lane_pull(a[j], gb + p), l, a[j]);
+                if (j < n) a[j] = fma(-row_bcast<k>(a[j]), l, a[j]);
         }
-    }
+    });
     return fail;
 }
 
-// solve (I - gamma J) x = b with q_lu's factors; b and x in component order (lane gl)
+// solve (I - gamma J) x = b with q_lu's factors (denseGETRS): b interchanged (P b: one bpermute),
+// forward with the unit L, backward with U; each step's pivot value reaches the row by a DPP
+// broadcast from the compile-time lane k. b and x in component order (lane gl).
 template <int NM>
-__device__ __forceinline__ double q_solve(const double (&a)[NM], int pstep, const int (&pk)[NM], double dinv, int n, int gl,
-                                          double b) {
+__device__ __forceinline__ double q_solve(const double (&a)[NM], int orig, double dinv, int n, int gl, double b) {
     const int gb = (int)(threadIdx.x & 48);
-    double y = gl < n ? b : 0.0;
-#pragma unroll
-    for (int k = 0; k < NM; ++k) {                       // L y = P b, in step order
+    double y = lane_pull(gl < n ? b : 0.0, gb + orig);
+    sfor<0, NM>([&](auto kc) {                                        // L y = P b
+        constexpr int k = decltype(kc)::value;
         if (k + 1 < n) {
-            const double yk = lane_pull(y, gb + pk[k]);
-            y = fma(-((pstep > k) ? a[k] : 0.0), yk, y);
+            const double yk = row_bcast<k>(y);
+            y = fma(-((gl > k) ? a[k] : 0.0), yk, y);
         }
-    }
+    });
     double x = 0.0;
-#pragma unroll
-    for (int j = NM - 1; j >= 0; --j) {                  // U x = y, steps n-1 .. 0
-        if (j < n) {
-            if (pstep == j) x = y * dinv;
-            const double xj = lane_pull(x, gb + pk[j]);
-            y = fma(-((pstep < j) ? a[j] : 0.0), xj, y);
+    sfor<0, NM>([&](auto kc) {                                        // U x = y, k = n-1 .. 0
+        constexpr int k = NM - 1 - decltype(kc)::value;
+        if (k < n) {
+            if (gl == k) x = y * dinv;
+            const double xk = row_bcast<k>(x);
+            y = fma(-((gl < k) ? a[k] : 0.0), xk, y);
         }
-    }
-    // x of unknown j sits on the lane that pivoted step j: send it to lane j
-    const int dst = (gl < n) ? gb + pstep : (int)(threadIdx.x & 63);
-    const long long xb = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_ds_permute(dst * 4, (int)(xb & 0xffffffffLL));
-    const int hi = __builtin_amdgcn_ds_permute(dst * 4, (int)(xb >> 32));
-    return gl < n ? __longlong_as_double(((long long)hi << 32) | (unsigned int)lo) : 0.0;
+    });
+    return gl < n ? x : 0.0;
+}
+
+// the controller entry points for 16-lane groups (BR_QCTL_NOINLINE: out of line, so their register
+// allocation is separate from the hot loop's)
+#ifndef BR_QCTL_NOINLINE
+#define BR_QCTL_NOINLINE 0
+#endif
+#if BR_QCTL_NOINLINE
+#define BR_QCTL_ATTR __noinline__
+#else
+#define BR_QCTL_ATTR __forceinline__
+#endif
+__device__ BR_QCTL_ATTR int q_post_rhs(LCtl* C, VT<1, 16>& V, int gl, const double (&f)[1], double (&b)[1]) {
+    return ctl_post_rhs<1, 16>(C, V, gl, f, b);
+}
+__device__ BR_QCTL_ATTR int q_post_solve(LCtl* C, VT<1, 16>& V, int gl, double (&delta)[1], int lu_fail) {
+    return ctl_post_solve<1, 16>(C, V, gl, delta, lu_fail);
 }
 
 #ifndef BR_QWPB
 #define BR_QWPB 4   // waves per workgroup (16 reactors); tables staged once per workgroup
 #endif
+#ifndef BR_QWPE
+#define BR_QWPE 3   // waves per SIMD the register allocation targets (<= 168 VGPRs)
+#endif
 
 // the quad integrator kernel: persistent grid, every group takes reactor indices from o.work
 template <int NM>
-__global__ __launch_bounds__(64 * BR_QWPB) void k_quad(DevMech M, int N, const double* __restrict__ Tv,
+__global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR_QWPE))) void k_quad(DevMech M, int N, const double* __restrict__ Tv,
                                                         double* __restrict__ U, const double* __restrict__ tfv, KOpts o,
                                                         double* __restrict__ stats, double* __restrict__ Jws) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -364,12 +399,12 @@ __global__ __launch_bounds__(64 * BR_QWPB) void k_quad(DevMech M, int N, const d
     int rid = take();
     double T = 0.0;
     bool fresh = true;
+    int dqj = -1;   // >= 0: building column dqj of the DQ Jacobian
     double a[NM];
-    int pk[NM];
-    int pstep = 1024;
+    int orig = gl;
     double dinv = 0.0;
 #pragma unroll
-    for (int j = 0; j < NM; ++j) { a[j] = 0.0; pk[j] = 0; }
+    for (int j = 0; j < NM; ++j) a[j] = 0.0;
     unsigned long long cyc0 = 0;
     for (;;) {
         if (__ballot(rid < N) == 0) break;
@@ -422,14 +457,44 @@ __global__ __launch_bounds__(64 * BR_QWPB) void k_quad(DevMech M, int N, const d
                 }
                 wave_sync();
             }
-            // ---- one RHS for this group's reactor, then its controller
-            const double yv = V.at(V_Y, 0);
+            // ---- one RHS for this group's reactor, then its controller. dqj >= 0: this RHS is at
+            // y + inc_dqj e_dqj, column dqj of CVODE's DQ Jacobian (cvLsDenseDQJac, k_integrate's
+            // dq_* steps with 16-lane groups)
+            double yv = V.at(V_Y, 0);
+            if (dqj >= 0) {
+                double inc[1];
+                dq_incs<1, quad::G>(C, V, gl, inc);
+                if (gl == dqj) yv += inc[0];
+            }
             const double fv = q_rhs<NM>(tb, sp, kd, fod, T, yv, gl, p_last);
             double f[1] = {fv}, b[1];
-            int act_code = ctl_post_rhs<1, quad::G>(C, V, gl, f, b);
+            int act_code;
+            bool jac_ready = false;
+            if (dqj >= 0) {
+                double inc[1];
+                dq_incs<1, quad::G>(C, V, gl, inc);
+                const double ii = 1.0 / gbcast<quad::G>(inc[0], dqj);
+                Jq[dqj * quad::G + gl] = ii * fv - ii * V.at(V_TEMP, 0);
+                C->nfe_dq = C->nfe_dq + 1;
+                if (++dqj < n) {
+                    act_code = A_RHS;
+                } else {
+                    dqj = -1;
+                    dq_newton_rhs<1, quad::G>(C, V, gl, b);
+                    act_code = A_SETUP;
+                    jac_ready = true;
+                }
+            } else {
+                act_code = q_post_rhs(C, V, gl, f, b);
+                if (act_code == A_SETUP && o.dq_jac && C->newj) {
+                    dq_begin<1, quad::G>(C, V, gl, f);
+                    dqj = 0;
+                    act_code = A_RHS;
+                }
+            }
             int lu_fail = 0;
             if (act_code == A_SETUP) {
-                if (C->newj) {                                        // analytic Jacobian at y, saved
+                if (!jac_ready && C->newj) {                          // analytic Jacobian at y, saved
                     double jr[NM];
                     q_jac<NM>(tb, sp, kd, fod, gl, jr);
 #pragma unroll
@@ -438,12 +503,12 @@ __global__ __launch_bounds__(64 * BR_QWPB) void k_quad(DevMech M, int N, const d
                 double jr[NM];
 #pragma unroll
                 for (int j = 0; j < NM; ++j) jr[j] = Jq[j * quad::G + gl];
-                lu_fail = q_lu<NM>(jr, C->gamma, n, gl, a, pstep, pk, dinv);
+                lu_fail = q_lu<NM>(jr, C->gamma, n, gl, a, orig, dinv);
             }
             if (act_code == A_SOLVE || act_code == A_SETUP) {
                 double delta[1] = {0.0};
-                if (!lu_fail) delta[0] = q_solve<NM>(a, pstep, pk, dinv, n, gl, b[0]);
-                act_code = ctl_post_solve<1, quad::G>(C, V, gl, delta, lu_fail);
+                if (!lu_fail) delta[0] = q_solve<NM>(a, orig, dinv, n, gl, b[0]);
+                act_code = q_post_solve(C, V, gl, delta, lu_fail);
             }
             if (act_code == A_DONE) {                                 // ---- results, next reactor
                 const int status = C->status;
@@ -457,7 +522,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) void k_quad(DevMech M, int N, const d
                     st[9] = st[10] = st[11] = st[12] = st[14] = st[15] = 0.0;
                     st[13] = C->tn;
                     st[16] = o.ign >= 0 ? (double)C->t_ign : NAN; st[17] = o.ign >= 0 ? (double)C->ign_rate : NAN;
-                    st[18] = o.ign >= 0 ? (double)C->ign_dt : NAN; st[19] = 0.0;
+                    st[18] = o.ign >= 0 ? (double)C->ign_dt : NAN; st[19] = C->nfe_dq;
                 }
                 rid = take();
                 fresh = true;

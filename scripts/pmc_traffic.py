@@ -16,7 +16,7 @@ import sys
 def total(path, name):
     s = 0.0
     for r in csv.DictReader(open(path)):
-        if ("k_integrate" in r["Kernel_Name"] or "k_lane" in r["Kernel_Name"]) and r["Counter_Name"] == name:
+        if any(k in r["Kernel_Name"] for k in ("k_integrate", "k_lane", "k_quad")) and r["Counter_Name"] == name:
             s += float(r["Counter_Value"])
     return s
 
@@ -30,7 +30,7 @@ def main():
     res = {"reactors": n, "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
            "read_bytes_corrected": rd, "write_bytes": wr,
            "bytes_per_reactor": (rd + wr) / n,
-           "note": "FETCH_SIZE x2 (gfx950 correction), KiB->B; integrator dispatches (k_integrate / k_lane) only"}
+           "note": "FETCH_SIZE x2 (gfx950 correction), KiB->B; integrator dispatches (k_integrate / k_lane / k_quad) only"}
     if len(sys.argv) > 5:
         hit = total(sys.argv[5], "TCC_HIT_sum")
         miss = total(sys.argv[5], "TCC_MISS_sum")

@@ -696,6 +696,40 @@ def test_quad_engine_h2o2(pkg, orc, gpu, monkeypatch):
     assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
 
 
+def test_quad_engine_dq_jacobian(pkg, orc, gpu, monkeypatch):
+    """k_quad with CVODE's DQ Jacobian (br_opts.dq_jacobian, the reference's setting): n RHS per
+    Jacobian counted in nfe_dq, states at the 28 output times within the H2/O2-DQ bounds of
+    test_integrate_parity against the oracle's cvLsDenseDQJac run, the same ignition time and step
+    counts; tight tolerances: end states to 1e-6 relative."""
+    monkeypatch.setenv("BRHIP_ENGINE", "quad")
+    from batchreactor_amd import ensemble
+    pm, om = _mechs(pkg, orc, "h2o2")
+    eng = pkg.Engine(pm)
+    assert eng.engine == "quad"
+    N = 128
+    T, Asv, U0 = ensemble.make_inputs(pm, "h2o2", 0, N)
+    U, st = eng.integrate(T, Asv, U0, 10.0, tout=OUT_T, dq_jacobian=True)
+    assert np.all(st["status"] == 0)
+    assert np.all(st["nfe_dq"] == st["nje"] * pm.n)
+    bounds = BOUNDS[("h2o2", True)]
+    nst_o = 0
+    for i in range(N):
+        uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], 10.0, OUT_T, analytic_jac=False)
+        ti = so["t_ign"]
+        assert abs(st["t_ign"][i] - ti) <= bounds[3] * max(st["ign_dt"][i], so["ign_dt"]) + 1e-4 * ti, i
+        eb = _band_errors(st["yout"][i], Yo, ti)
+        for w, (bound, e) in enumerate(zip(bounds[:3], eb)):
+            assert e <= bound, (i, ("pre", "front", "post")[w], e, bound)
+        nst_o += so["nsteps"]
+    assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
+    T, Asv, U0 = _ignition_inputs(pm, "h2o2", 64, 6)
+    U, st = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16, dq_jacobian=True)
+    assert np.all(st["status"] == 0)
+    for i in range(64):
+        uo, so, _ = om.integrate(T[i], Asv[i], U0[i], 1e-2, analytic_jac=False, rtol=1e-10, atol=1e-16)
+        assert close_states(U[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, i
+
+
 def test_quad_engine_step_budget_and_wave_agreement(pkg, orc, gpu, monkeypatch):
     """k_quad: max_steps = 60 stops every reactor that needs more with BR_ERR_MAXSTEPS (-1) after
     exactly 60 steps, as the oracle's CVODE run; and the quad and wavefront engines (same
