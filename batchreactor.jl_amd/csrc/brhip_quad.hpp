@@ -406,12 +406,24 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
 #pragma unroll
     for (int j = 0; j < NM; ++j) a[j] = 0.0;
     unsigned long long cyc0 = 0;
+#if BR_PHASE_CLOCKS   // diagnostic build: this group's shader clocks per phase (br_stats cyc_*)
+    unsigned long long q_rhs_c = 0, q_jac_c = 0, q_lu_c = 0, q_sol_c = 0, q_ctl_c = 0, q_all = 0;
+#define QCLK(v) const unsigned long long v = clock64()
+#define QACC(acc, v) acc += clock64() - v
+#else
+#define QCLK(v)
+#define QACC(acc, v)
+#endif
     for (;;) {
         if (__ballot(rid < N) == 0) break;
         if (rid < N) {
             if (fresh) {                                              // ---- CVodeInit for reactor rid
                 fresh = false;
                 cyc0 = wall_clock64();
+#if BR_PHASE_CLOCKS
+                q_rhs_c = q_jac_c = q_lu_c = q_sol_c = q_ctl_c = 0;
+                q_all = clock64();
+#endif
                 T = Tv[rid];
                 C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
                 C->a_max_steps = o.max_steps; C->a_trace_cap = 0; C->a_trace = nullptr; C->a_rid = rid; C->a_n = n;
@@ -466,10 +478,13 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
                 dq_incs<1, quad::G>(C, V, gl, inc);
                 if (gl == dqj) yv += inc[0];
             }
+            QCLK(c_r);
             const double fv = q_rhs<NM>(tb, sp, kd, fod, T, yv, gl, p_last);
+            QACC(q_rhs_c, c_r);
             double f[1] = {fv}, b[1];
             int act_code;
             bool jac_ready = false;
+            QCLK(c_c);
             if (dqj >= 0) {
                 double inc[1];
                 dq_incs<1, quad::G>(C, V, gl, inc);
@@ -492,23 +507,32 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
                     act_code = A_RHS;
                 }
             }
+            QACC(q_ctl_c, c_c);
             int lu_fail = 0;
             if (act_code == A_SETUP) {
                 if (!jac_ready && C->newj) {                          // analytic Jacobian at y, saved
+                    QCLK(c_j);
                     double jr[NM];
                     q_jac<NM>(tb, sp, kd, fod, gl, jr);
 #pragma unroll
                     for (int j = 0; j < NM; ++j) Jq[j * quad::G + gl] = jr[j];
+                    QACC(q_jac_c, c_j);
                 }
+                QCLK(c_l);
                 double jr[NM];
 #pragma unroll
                 for (int j = 0; j < NM; ++j) jr[j] = Jq[j * quad::G + gl];
                 lu_fail = q_lu<NM>(jr, C->gamma, n, gl, a, orig, dinv);
+                QACC(q_lu_c, c_l);
             }
             if (act_code == A_SOLVE || act_code == A_SETUP) {
+                QCLK(c_s);
                 double delta[1] = {0.0};
                 if (!lu_fail) delta[0] = q_solve<NM>(a, orig, dinv, n, gl, b[0]);
+                QACC(q_sol_c, c_s);
+                QCLK(c_p);
                 act_code = q_post_solve(C, V, gl, delta, lu_fail);
+                QACC(q_ctl_c, c_p);
             }
             if (act_code == A_DONE) {                                 // ---- results, next reactor
                 const int status = C->status;
@@ -519,7 +543,12 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
                     st[0] = C->nst; st[1] = C->nfe; st[2] = C->nje; st[3] = C->nsetups; st[4] = C->nni;
                     st[5] = C->ncfn; st[6] = C->netf; st[7] = (double)status;
                     st[8] = (double)(wall_clock64() - cyc0);
+#if BR_PHASE_CLOCKS
+                    st[9] = (double)q_rhs_c; st[10] = (double)q_jac_c; st[11] = (double)q_lu_c; st[12] = (double)q_sol_c;
+                    st[14] = (double)q_ctl_c; st[15] = (double)(clock64() - q_all);
+#else
                     st[9] = st[10] = st[11] = st[12] = st[14] = st[15] = 0.0;
+#endif
                     st[13] = C->tn;
                     st[16] = o.ign >= 0 ? (double)C->t_ign : NAN; st[17] = o.ign >= 0 ? (double)C->ign_rate : NAN;
                     st[18] = o.ign >= 0 ? (double)C->ign_dt : NAN; st[19] = C->nfe_dq;

@@ -196,7 +196,7 @@ def test_integrate_parity(pkg, orc, gpu, case, N, dq):
     (tests/parity_bands.py: 2x the oracle's own rounding spread across and after the front), the same
     step count to 35 % per reactor and 3 % over the slice (rounding changes step sequences).
     Both engines use the analytic Jacobian by default; the "-dq" cases run CVODE's DQ Jacobian
-    (br_opts.dq_jacobian, the reference's setting: the lane engine for H2/O2, the wavefront engine
+    (br_opts.dq_jacobian, the reference's setting: the quad engine for H2/O2, the wavefront engine
     for GRI and gas+surface) against the oracle's DQ run."""
     from batchreactor_amd import ensemble
     pm, om = _mechs(pkg, orc, case)
@@ -615,7 +615,7 @@ def test_lane_engine_h2o2(pkg, orc, gpu, monkeypatch):
     per wave, so lanes take new reactors from the work counter mid-run. Tight tolerances: end
     states agree to 1e-6 relative; default tolerances: same status and, summed over the
     ensemble, the same step / RHS / Jacobian counts to 10 % (rounding changes step sequences)."""
-    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    monkeypatch.setenv("BRHIP_ENGINE", "lane")
     pm, om = _mechs(pkg, orc, "h2o2")
     eng = pkg.Engine(pm)
     assert eng.engine == "lane"
@@ -646,7 +646,7 @@ def test_lane_and_wave_engines_agree(pkg, gpu, monkeypatch):
     same H2/O2 end states at tight tolerances."""
     pm = pkg.Mechanism.from_files(LIB, gas_mech="h2o2.dat")
     T, Asv, U0 = _ignition_inputs(pm, "h2o2", 96, 8)
-    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    monkeypatch.setenv("BRHIP_ENGINE", "lane")
     eng = pkg.Engine(pm)
     assert eng.engine == "lane"
     Ul, sl = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
@@ -758,7 +758,7 @@ def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
     most of the 300 reactors take that path; every end state must still match the oracle at tight
     tolerances, the step counts must be the full ones (lane + wave), and dense output rows written
     by either engine must match the oracle."""
-    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    monkeypatch.setenv("BRHIP_ENGINE", "lane")
     monkeypatch.setenv("BRHIP_DEFER_STEPS", "30")
     pm, om = _mechs(pkg, orc, "h2o2")
     eng = pkg.Engine(pm)
@@ -785,7 +785,7 @@ def test_lane_deferral_step_budget(pkg, orc, gpu, monkeypatch):
     maxiters counts every step of one solve): with max_steps = 60 and deferral after 30 lane steps,
     every reactor that needs more than 60 steps stops with BR_ERR_MAXSTEPS (-1) after exactly 60
     steps in total -- the oracle's CVODE run reports the same status at the same step count."""
-    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    monkeypatch.setenv("BRHIP_ENGINE", "lane")
     monkeypatch.setenv("BRHIP_DEFER_STEPS", "30")
     pm, om = _mechs(pkg, orc, "h2o2")
     eng = pkg.Engine(pm)
