@@ -199,11 +199,12 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
 // surface-only +2.7 %, round 3)
 __device__ __forceinline__ double ud(const LDbl& x) { return (double)x; }
 __device__ __forceinline__ int ui(const __attribute__((address_space(3))) int& x) { return uni((int)x); }
-// Reactor groups: the wavefront engine runs one reactor per wave (group width GW = 64); the quad
-// engine (brhip_quad.hpp) four per wave, one per 16-lane DPP row (GW = 16), with `lane` the lane
-// within the group. The controller's values are uniform per group: scalar for GW = 64
-// (readfirstlane: SGPRs, scalar branches), per-lane VGPRs with exec-masked branches for GW = 16;
-// reductions and broadcasts over the group (DPP row butterflies, ds_bpermute inside the row).
+// Reactor groups: the wavefront engine runs one reactor per wave (group width GW = 64); the group
+// engines (brhip_quad.hpp) two or four per wave, one per 32-lane half or 16-lane DPP row (GW = 32 /
+// 16), with `lane` the lane within the group. The controller's values are uniform per group: scalar
+// for GW = 64 (readfirstlane: SGPRs, scalar branches), per-lane VGPRs with exec-masked branches for
+// GW < 64; reductions and broadcasts over the group (DPP row butterflies, permlane16 swaps between
+// the rows of a half, ds_bpermute inside the group).
 template <int GW>
 __device__ __forceinline__ int gui(const __attribute__((address_space(3))) int& x) {
     if constexpr (GW == 64) return uni((int)x);
@@ -222,18 +223,20 @@ __device__ __forceinline__ double guni(double v) {
 template <int GW>
 __device__ __forceinline__ double gsum(double v) {
     if constexpr (GW == 64) return wave_sum(v);
+    else if constexpr (GW == 32) return half_sum(v);
     else return row_sum(v);
 }
 template <int GW>
 __device__ __forceinline__ double gmax(double v) {
     if constexpr (GW == 64) return wave_max(v);
+    else if constexpr (GW == 32) return half_max(v);
     else return row_max(v);
 }
 // value of v in lane k of the group (k uniform per group)
 template <int GW>
 __device__ __forceinline__ double gbcast(double v, int k) {
     if constexpr (GW == 64) return bcast(v, k);
-    else return lane_pull(v, (int)(threadIdx.x & 48) + k);
+    else return lane_pull(v, (int)(threadIdx.x & (64 - GW)) + k);
 }
 
 #ifndef BR_CTL_INLINE
@@ -1037,7 +1040,7 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane,
 }
 
 #include "brhip_lane.hpp"   // one reactor per lane (small gas mechanisms)
-#include "brhip_quad.hpp"   // four reactors per wave, one per 16-lane DPP row (small gas mechanisms)
+#include "brhip_quad.hpp"   // group engines: 4 / 2 reactors per wave (16- / 32-lane groups, n <= 32)
 
 // ------------------------------------------------------------------------------------
 // the integrator kernel: one reactor per 64-lane wavefront, `rpb` reactors per workgroup
@@ -1405,6 +1408,12 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
+// the group-engine instances (brhip_quad.hpp)
+static const void* grp_kernel(int gl, int nm) {
+    if (gl == 16) return nm == 9 ? (const void*)k_group<16, 9> : (const void*)k_group<16, 16>;
+    return nm == 24 ? (const void*)k_group<32, 24> : (const void*)k_group<32, 32>;
+}
+
 struct br_mech {
     int device = 0;
     int ng = 0, ns = 0, nrg = 0, nrs = 0, n = 0, nmax = 64, rpb = 1, waves_per_cu = 0;
@@ -1425,9 +1434,10 @@ struct br_mech {
     double* lws = nullptr;     // saved Jacobians, slot-major [NM*NM][slots]
     size_t lws_bytes = 0;
     int* queue = nullptr;      // work counter
-    // four-reactors-per-wave engine (brhip_quad.hpp): 0 = not eligible, else the register width NM
-    int quad_nm = 0, quad_blocks = 0;
-    size_t quad_shmem = 0;
+    // group engine (brhip_quad.hpp): gl = 0 not eligible, else the group width (16: quad, 32: pair)
+    // and the register width NM of k_group<gl, NM>
+    int grp_gl = 0, grp_nm = 0, grp_blocks = 0;
+    size_t grp_shmem = 0;
     double* qws = nullptr;     // saved Jacobians, 16 x 16 per group slot
     size_t qws_bytes = 0;
     int* wq = nullptr;         // k_integrate work counter
@@ -1476,19 +1486,25 @@ int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs) {
     return 0;
 }
 
-// engine selection for br_integrate* (untraced): BRHIP_ENGINE = wave | lane | quad forces one (when
-// the mechanism is eligible); default: the quad engine for eligible mechanisms (BR_QUAD_DEFAULT; C2
-// H2/O2 882k reactors/s against 477k for the lane engine and 470k for the wavefront engine, round 4),
-// else the lane engine, else the wavefront engine
+// engine selection for br_integrate* (untraced): BRHIP_ENGINE = wave | lane | quad | pair forces one
+// (when the mechanism is eligible); default: the group engine for eligible mechanisms (quad, n <= 16:
+// C2 H2/O2 882k reactors/s against 477k for the lane engine and 470k for the wavefront engine, round
+// 4; pair, 16 < n <= 32, when BR_PAIR_DEFAULT: off, surface-only Ni/CH4 194.8k vs 217.7k for the
+// wavefront engine), else the lane engine, else the wavefront engine.
+// Codes: 0 wavefront, NM > 0 lane, -(100 gl + NM) group.
 #ifndef BR_QUAD_DEFAULT
 #define BR_QUAD_DEFAULT 1
+#endif
+#ifndef BR_PAIR_DEFAULT
+#define BR_PAIR_DEFAULT 0
 #endif
 static int pick_engine(const br_mech* m) {
     const char* eng = getenv("BRHIP_ENGINE");
     if (eng && strcmp(eng, "wave") == 0) return 0;
     if (eng && strcmp(eng, "lane") == 0) return m->lane_nm;
-    const bool want_quad = (eng && strcmp(eng, "quad") == 0) || BR_QUAD_DEFAULT;
-    if (m->quad_nm && want_quad) return -m->quad_nm;
+    const int gcode = -(100 * m->grp_gl + m->grp_nm);
+    if (m->grp_gl == 16 && ((eng && strcmp(eng, "quad") == 0) || (!eng && BR_QUAD_DEFAULT))) return gcode;
+    if (m->grp_gl == 32 && ((eng && strcmp(eng, "pair") == 0) || (!eng && BR_PAIR_DEFAULT))) return gcode;
     return m->lane_nm;
 }
 int br_mech_engine(const br_mech* m) {
@@ -1851,19 +1867,20 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
             m->lane_blocks = nb * ncu;
         }
     }
-    // ---- four reactors per wave for small gas-only mechanisms (brhip_quad.hpp)
-    if (ns == 0 && n <= 16 && M.nset <= quad::MAX_SETS) {
-        m->quad_nm = n <= 9 ? 9 : 16;
-        const void* qfn = m->quad_nm == 9 ? (const void*)k_quad<9> : (const void*)k_quad<16>;
-        m->quad_shmem = (size_t)M.img_bytes + (size_t)BR_QWPB * 4 * quad::block_bytes(nrg, M.nfo);
+    // ---- group engines (brhip_quad.hpp): 4 reactors per wave for n <= 16, 2 for n <= 32
+    if (n <= 32 && M.nset <= grp::MAX_SETS) {
+        m->grp_gl = n <= 16 ? 16 : 32;
+        m->grp_nm = n <= 9 ? 9 : (n <= 16 ? 16 : (n <= 24 ? 24 : 32));
+        const void* gfn = grp_kernel(m->grp_gl, m->grp_nm);
+        m->grp_shmem = (size_t)M.img_bytes + (size_t)BR_QWPB * (64 / m->grp_gl) * grp::block_bytes(m->grp_gl, nrg, M.nfo, nrs);
         int nb = 0;
-        if (m->quad_shmem > LDS_PER_CU ||
-            hipFuncSetAttribute(qfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->quad_shmem) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, qfn, 64 * BR_QWPB, m->quad_shmem) != hipSuccess || nb <= 0) {
-            m->quad_nm = 0;
+        if (m->grp_shmem > LDS_PER_CU ||
+            hipFuncSetAttribute(gfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->grp_shmem) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gfn, 64 * BR_QWPB, m->grp_shmem) != hipSuccess || nb <= 0) {
+            m->grp_gl = m->grp_nm = 0;
         } else {
-            nb = std::min(nb, (int)(LDS_PER_CU / ((m->quad_shmem + LDS_GRANULE - 1) / LDS_GRANULE * LDS_GRANULE)));
-            m->quad_blocks = nb * m->ncu;
+            nb = std::min(nb, (int)(LDS_PER_CU / ((m->grp_shmem + LDS_GRANULE - 1) / LDS_GRANULE * LDS_GRANULE)));
+            m->grp_blocks = nb * m->ncu;
         }
     }
     HIPCHK(hipEventCreate(&m->ev0));
@@ -2025,12 +2042,12 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
     hipStream_t s = (hipStream_t)stream;
     const int engine = trace ? 0 : pick_engine(m);   // traced runs: the wavefront engine
     if (engine < 0) {
-        // four reactors per wave (one per 16-lane row), persistent grid over the resident
+        // 2 or 4 reactors per wave (one per 32- / 16-lane group), persistent grid over the resident
         // workgroups, reactors from a work counter
-        const int NM = -engine;
-        const int gpb = BR_QWPB * 4;
-        const int blocks = std::max(1, std::min((N + gpb - 1) / gpb, m->quad_blocks));
-        const size_t need = (size_t)blocks * gpb * quad::G * quad::G * sizeof(double);
+        const int GL = m->grp_gl;
+        const int gpb = BR_QWPB * (64 / GL);
+        const int blocks = std::max(1, std::min((N + gpb - 1) / gpb, m->grp_blocks));
+        const size_t need = (size_t)blocks * gpb * GL * GL * sizeof(double);
         if (m->qws_bytes < need) {
             if (m->qws) hipFree(m->qws);
             m->qws = nullptr; m->qws_bytes = 0;
@@ -2040,15 +2057,14 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
         if (!m->queue) HIPCHK(hipMalloc((void**)&m->queue, (2 + DEFER_CAP) * sizeof(int)));
         HIPCHK(hipMemsetAsync(m->queue, 0, 2 * sizeof(int), s));
         o.work = m->queue;
+        const void* gfn = grp_kernel(GL, m->grp_nm);
+        HIPCHK(hipFuncSetAttribute(gfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->grp_shmem));
         HIPCHK(hipEventRecord(m->ev0, s));
-        if (NM == 9) {
-            HIPCHK(hipFuncSetAttribute((const void*)k_quad<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->quad_shmem));
-            hipLaunchKernelGGL(k_quad<9>, dim3(blocks), dim3(64 * BR_QWPB), m->quad_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->qws);
-        } else {
-            HIPCHK(hipFuncSetAttribute((const void*)k_quad<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->quad_shmem));
-            hipLaunchKernelGGL(k_quad<16>, dim3(blocks), dim3(64 * BR_QWPB), m->quad_shmem, s, m->dm, N, dT, du, dtf, o, (double*)dstats, m->qws);
-        }
-        HIPCHK(hipGetLastError());
+        const DevMech dm = m->dm;
+        double* st_ = (double*)dstats;
+        double* qws = m->qws;
+        void* args[] = {(void*)&dm, (void*)&N, (void*)&dT, (void*)&dAsv, (void*)&du, (void*)&dtf, (void*)&o, (void*)&st_, (void*)&qws};
+        HIPCHK(hipLaunchKernel(gfn, dim3(blocks), dim3(64 * BR_QWPB), args, m->grp_shmem, s));
         HIPCHK(hipEventRecord(m->ev1, s));
         m->ev_recorded = true;
         return 0;

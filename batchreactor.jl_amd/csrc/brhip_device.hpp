@@ -250,6 +250,30 @@ __device__ __forceinline__ double row_max(double v) {
     v = fmax(v, dppd<0x140>(v));
     return v;
 }
+// the two 16-lane rows of each 32-lane half: v_permlane16_swap (gfx950) of a value with itself gives
+// every lane its half's even-row value (.even) and odd-row value (.odd)
+struct RowPair {
+    double even, odd;
+};
+__device__ __forceinline__ RowPair row_pair(double v) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((int)(b & 0xffffffffLL), (int)(b & 0xffffffffLL), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    RowPair r;
+    r.even = __longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]);
+    r.odd = __longlong_as_double(((long long)hi[1] << 32) | (unsigned int)lo[1]);
+    return r;
+}
+// sum / max over each 32-lane half (the pair engine's reactor groups): the row butterflies, then the
+// two row results combined in the same order on every lane (even + odd)
+__device__ __forceinline__ double half_sum(double v) {
+    const RowPair p = row_pair(row_sum(v));
+    return p.even + p.odd;
+}
+__device__ __forceinline__ double half_max(double v) {
+    const RowPair p = row_pair(row_max(v));
+    return fmax(p.even, p.odd);
+}
 
 // opaque copy of a uniform pointer: addresses derived from it cannot be hoisted out of the
 // integrator's main loop (otherwise LICM keeps ~NMAX 64-bit column addresses live across the

@@ -1,34 +1,45 @@
-// brhip_quad.hpp -- FOUR REACTORS PER WAVE integrator for small gas-phase mechanisms (n <= 16
-// components, no surface species; e.g. H2/O2, n = 9, the C2 ensemble). Included by brhip.hip after
-// the controller: it runs the same CVODE 5.x restatement (begin_step / ctl_post_rhs /
-// ctl_post_solve, src/BatchReactor.jl:138-141,:210) with the controller instantiated for 16-lane
-// reactor groups (GW = 16).
+// brhip_quad.hpp -- GROUP ENGINES: two or four reactors per wave for small mechanisms. A reactor
+// occupies a group of GL lanes (GL = 16: one DPP row, n <= 16, "quad", e.g. H2/O2 n = 9, the C2
+// ensemble; GL = 32: one half-wave, 16 < n <= 32, "pair", e.g. the surface-only Ni/CH4 case, n = 20,
+// C4), lane gl of the group holds component gl. Included by brhip.hip after the controller: the same
+// CVODE 5.x restatement (begin_step / ctl_post_rhs / ctl_post_solve, src/BatchReactor.jl:138-141,
+// :210) runs with the controller instantiated for GL-lane groups (GW = GL).
 //
-// Why: one reactor per wave leaves 55 of 64 lanes idle for H2/O2 (n = 9, 27 reactions) in the LU
-// and solve and pays the ~1k-instruction step controller per reactor; one reactor per lane
-// (k_lane) keeps a reactor's whole state in one lane's registers (436 registers, 1 wave/SIMD,
-// spills, 2.6 MB of memory traffic per reactor) and runs every controller branch of 64 diverging
-// reactors. Here reactor g of a wave sits on the 16-lane DPP row g, lane gl = lane & 15 holds
-// component gl: the controller is shared by 4 reactors (4-way divergence), reductions are DPP row
-// butterflies, the LU factors live in registers (one row per lane), the solve needs no memory.
+// Why: one reactor per wave leaves most lanes idle for small n in every per-component operation
+// and pays the step controller (~1k instructions) per reactor; one reactor per lane (k_lane) keeps
+// a reactor's whole state in one lane's registers (436 registers, 1 wave/SIMD, spills, 2.6 MB of
+// memory traffic per H2/O2 reactor) and runs every controller branch of 64 diverging reactors. Here
+// the controller serves 2 or 4 reactors per instruction (2- or 4-way divergence at most), group
+// reductions are DPP row butterflies (plus one permlane16 swap for 32-lane groups), the LU factors
+// live in registers (one row per lane) and the solve needs no memory.
 //
-// Per reactor (LDS): [Ctl | V: NVEC x 16 doubles | species block: conc[0..15], acc[16..31],
-// mc[32..63], 1.0 at [64] (the records' pad species SP_ONE = 64) | kd: {kf, kr} per reaction | fod:
-// {k0/kinf, log10 Fcent, c, n} per falloff reaction]. Global: the saved Jacobian, 16 x 16
-// column-major per reactor slot. Mechanism tables as for the wavefront engine (LDS image).
+// Per reactor (LDS): [Ctl | V: NVEC x GL doubles | species block (GLay) | kd: {kf, kr} per gas
+// reaction | fod: {k0/kinf, log10 Fcent, c, n} per falloff reaction | skd: k(T) per surface
+// reaction]. Global: the saved Jacobian, GL x GL column-major per group slot. Mechanism tables as for
+// the wavefront engine (LDS image, records with the pad species 64 = conc 1.0).
 #pragma once
 
-namespace quad {
-constexpr int G = 16;                               // lanes per reactor
-constexpr int SP_CONC = 0, SP_ACC = 16, SP_MC = 32, SP_ONE_Q = 64, SP_DOUBLES = 66;
-constexpr int MAX_SETS = 32;                        // mc[32..63]
-__host__ __device__ inline int vbytes() { return NVEC * G * 8; }
-__host__ __device__ inline int block_bytes(int nrg, int nfo) {
-    const int b = CTL_BYTES + vbytes() + SP_DOUBLES * 8 + 16 * nrg + 32 * nfo;
+namespace grp {
+// species block of a group (doubles): conc[CONC + k], gas production sums ACCW, surface production
+// sums ACCS, third-body sums MC (<= 32 efficiency sets), conc[ONE] = 1.0 (the records' pad species
+// Lay<1>::ONE = 64, so conc + 64 must land on it)
+template <int GL>
+struct GLay {
+    static constexpr int CONC = 0, ACCW = GL, ONE = 64, ACCS = 66;
+    static constexpr int MC = GL == 16 ? 32 : 98;
+    static constexpr int DOUBLES = GL == 16 ? 82 : 130;
+    static_assert(GL == 16 || GL == 32, "group width");
+    static_assert(ONE == Lay<1>::ONE, "pad species");
+};
+constexpr int MAX_SETS = 32;
+__host__ __device__ inline int vbytes(int gl) { return NVEC * gl * 8; }
+__host__ __device__ inline int sp_off(int gl) { return CTL_BYTES + vbytes(gl); }
+__host__ __device__ inline int kd_off(int gl) { return sp_off(gl) + (gl == 16 ? GLay<16>::DOUBLES : GLay<32>::DOUBLES) * 8; }
+__host__ __device__ inline int block_bytes(int gl, int nrg, int nfo, int nrs) {
+    const int b = kd_off(gl) + 16 * nrg + 32 * nfo + 8 * nrs;
     return (b + 15) / 16 * 16;
 }
-__host__ __device__ inline int kd_off() { return CTL_BYTES + vbytes() + SP_DOUBLES * 8; }
-}  // namespace quad
+}  // namespace grp
 
 // max of a 32-bit value over each 16-lane DPP row (every lane gets its row's max)
 __device__ __forceinline__ unsigned row_umax(unsigned x) {
@@ -47,15 +58,51 @@ __device__ __forceinline__ unsigned row_umax(unsigned x) {
         : "v"(x));
     return r;
 }
+// ... over each group (32-lane groups: the two row maxima exchanged by a permlane16 swap)
+template <int GL>
+__device__ __forceinline__ unsigned group_umax(unsigned x) {
+    const unsigned m = row_umax(x);
+    if constexpr (GL == 16) return m;
+    else {
+        const auto p = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+        return max((unsigned)p[0], (unsigned)p[1]);
+    }
+}
 
-// T-only constants of one group's reactor (init_tconst for the quad layout): {kf, kr} per gas
-// reaction into kd, falloff constants into fod; g/RT per species in the acc slots (scratch)
-template <int NM>
-__device__ __forceinline__ void q_init_tconst(const Tab& tb, double* sp, double* kd, double* fod, double T, int gl) {
+// compile-time loop: f(std::integral_constant<int, K>) for K = B .. E-1
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+// value of lane K of this lane's 16-lane row (DPP row_newbcast: a VALU move, no LDS crossbar)
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) { return dppd<0x150 + K>(v); }
+// value of lane K (compile time) of this lane's group: the row broadcast, and for 32-lane groups the
+// row holding lane K through a permlane16 swap
+template <int GL, int K>
+__device__ __forceinline__ double group_bcast(double v) {
+    const double r = row_bcast<K & 15>(v);
+    if constexpr (GL == 16) return r;
+    else {
+        const RowPair p = row_pair(r);
+        return K < 16 ? p.even : p.odd;
+    }
+}
+
+// T-only constants of one group's reactor (init_tconst for the group layout): {kf, kr} per gas
+// reaction into kd, falloff constants into fod, k(T) per surface reaction into skd; g/RT per gas
+// species in the ACCW slots (scratch)
+template <int GL>
+__device__ __forceinline__ void g_init_tconst(const Tab& tb, double* sp, double* kd, double* fod, double* skd, double T,
+                                              int gl) {
+    typedef grp::GLay<GL> L;
     const double lT = log(T);
-    double* grt = sp + quad::SP_ACC;
-    const int ng = MF(ng), nrg = MF(nrg);
-    if (gl == 0) sp[quad::SP_ONE_Q] = 1.0;
+    double* grt = sp + L::ACCW;
+    const int ng = MF(ng), nrg = MF(nrg), nrs = MF(nrs);
+    if (gl == 0) sp[L::ONE] = 1.0;
     if (gl < ng) {
         const double* c = MF(nasa) + 15 * gl;
         const double* a = (T < c[0]) ? c + 8 : c + 1;
@@ -66,7 +113,7 @@ __device__ __forceinline__ void q_init_tconst(const Tab& tb, double* sp, double*
     wave_sync();
     const double RT = R_GAS * T;
 #pragma unroll 1
-    for (int r = gl; r < nrg; r += quad::G) {
+    for (int r = gl; r < nrg; r += GL) {
         const auto rec = rx_rec(tb.rx, r);
         const uint32_t info = rec[2];
         const double* gp = MF(g_par) + 4 * r;
@@ -99,41 +146,57 @@ __device__ __forceinline__ void q_init_tconst(const Tab& tb, double* sp, double*
             fo[3] = 0.75 - 1.27 * lfc;
         }
     }
+#pragma unroll 1
+    for (int r = gl; r < nrs; r += GL) {                               // as init_tconst
+        const uint32_t info = tb.sx[SX_WORDS * r + 4];
+        const double* spr = MF(s_par) + 4 * r;
+        double k;
+        if (si_stick(info)) k = spr[0] * sqrt(RT / (2 * M_PI * spr[3]));
+        else k = spr[0] * pow(T, spr[1]) * exp(-spr[2] / RT);
+        skd[r] = k;
+    }
     wave_sync();
 }
 
 // the mass-action part kf prod(c_f) - kr prod(c_b) of gas reaction r of a group (products in the
-// wavefront engine's order; pad slots read conc[SP_ONE_Q] = 1), the reactant / product
-// concentrations kept for the Jacobian
-__device__ __forceinline__ double q_mass_action(const double* sp, const double* kd, uint32_t w0, uint32_t w1, int r,
+// wavefront engine's order; pad slots read conc[ONE] = 1), the reactant / product concentrations
+// kept for the Jacobian
+template <int GL>
+__device__ __forceinline__ double g_mass_action(const double* sp, const double* kd, uint32_t w0, uint32_t w1, int r,
                                                 double (&cf)[4], double (&cb)[4]) {
+    typedef grp::GLay<GL> L;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        cf[e] = sp[quad::SP_CONC + sp8(w0, e)];
-        cb[e] = sp[quad::SP_CONC + sp8(w1, e)];
+        cf[e] = sp[L::CONC + sp8(w0, e)];
+        cb[e] = sp[L::CONC + sp8(w1, e)];
     }
     double Pf = (cf[0] * cf[1]) * cf[2], Pb = (cb[0] * cb[1]) * cb[2];
     if (MF(nu4)) { Pf *= cf[3]; Pb *= cb[3]; }
     return kd[2 * r] * Pf - kd[2 * r + 1] * Pb;
 }
 
-// residual! (src/BatchReactor.jl:312-376) for a gas-only group: du of component gl; the pressure
-// of this evaluation to *p_out (save_data semantics)
-template <int NM>
-__device__ __forceinline__ double q_rhs(const Tab& tb, double* sp, const double* kd, const double* fod, double T, double u,
-                                        int gl, double* p_out) {
-    const int n = MF(n), nrg = MF(nrg), nset = MF(nset);
+// residual! (src/BatchReactor.jl:312-376) of a group's reactor: du of component gl (gas rates
+// :355, surface rates :344, du assembly with the Asv quirk :345,:363-373); the pressure of this
+// evaluation to *p_out (save_data semantics). Same arithmetic order as the wavefront engine's rhs()
+// (concentrations, third-body pairing, rate products, falloff, surface coverage factor).
+template <int GL>
+__device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const double* kd, const double* fod, const double* skd,
+                                        double T, double Asv, double Asv_th, double u, int gl, double* p_out) {
+    typedef grp::GLay<GL> L;
+    const int n = MF(n), ng = MF(ng), nrg = MF(nrg), nrs = MF(nrs), nset = MF(nset);
+    const bool gas = gl < ng;
     const double Mk = tb.molwt[gl];
-    const double c = gl < n ? u / Mk : 0.0;                         // c_k = u_k / M_k (p x_k / RT)
-    sp[quad::SP_CONC + gl] = c;
-    sp[quad::SP_ACC + gl] = 0.0;
-    const double Ctot = row_sum(c);
+    const double c = gl < n ? (gas ? u / Mk : u) : 0.0;              // c_k = u_k / M_k; coverages as is
+    sp[L::CONC + gl] = c;
+    sp[L::ACCW + gl] = 0.0;
+    if (nrs) sp[L::ACCS + gl] = 0.0;
+    const double Ctot = gsum<GL>(gas ? c : 0.0);
     const double p = R_GAS * T * Ctot;
     wave_sync();
-    const double* conc = sp + quad::SP_CONC;
+    const double* conc = sp + L::CONC;
 #pragma unroll 1
-    for (int t = gl; t < nset; t += quad::G) {                      // third-body sums per efficiency set
-        const uint32_t w = tb.tbs[t];                                // (pairing as third_body_sets)
+    for (int t = gl; t < nset; t += GL) {                              // third-body sums per efficiency set
+        const uint32_t w = tb.tbs[t];                                  // (pairing as third_body_sets)
         const int b = w & 0xFFFFF, e = b + (int)(w >> 20);
         double s0 = Ctot, s1 = 0.0;
         int i = b;
@@ -148,90 +211,119 @@ __device__ __forceinline__ double q_rhs(const Tab& tb, double* sp, const double*
             const double2 e0 = *reinterpret_cast<const double2*>(tb.tbe + 16 * i);
             s0 = fma(e0.y, conc[__double_as_longlong(e0.x) & 0xFFFF], s0);
         }
-        sp[quad::SP_MC + t] = s0 + s1;
+        sp[L::MC + t] = s0 + s1;
     }
     wave_sync();
-    double* acc = sp + quad::SP_ACC;
+    double* accw = sp + L::ACCW;
+    double* accs = sp + L::ACCS;
     const bool xm = (MF(conv) & 2) != 0;
 #pragma unroll 1
-    for (int r = gl; r < nrg; r += quad::G) {                        // reaction r on lane r mod 16
+    for (int r = gl; r < nrg; r += GL) {                               // gas reaction r on lane r mod GL
         const auto rr = rx_rec(tb.rx, r);
         const uint4 ra = *reinterpret_cast<const uint4*>(rr.a);
         const uint4 rb = *reinterpret_cast<const uint4*>(rr.b);
         double cf[4], cb[4];
-        double D = q_mass_action(sp, kd, ra.x, ra.y, r, cf, cb);
+        double D = g_mass_action<GL>(sp, kd, ra.x, ra.y, r, cf, cb);
         const int tbk = gi_tb(ra.z);
-        if (tbk) {                                                   // as production()'s rate
-            const double Mc = sp[quad::SP_MC + gi_tbidx(ra.z)];
+        if (tbk) {                                                     // as production()'s rate
+            const double Mc = sp[L::MC + gi_tbidx(ra.z)];
             if (tbk == 1) D *= Mc;
             else {
                 double fac, dfac;
                 falloff<false>(fod + 4 * gi_foidx(ra.z), gi_troe(ra.z) != 0, Mc, fac, dfac);
                 D *= fac;
-                if (xm) D *= Mc * 1e-6;                              // [M] in mol/cm3
+                if (xm) D *= Mc * 1e-6;                                // [M] in mol/cm3
             }
         }
-        scatter(acc, rb.x, rb.y, rb.z, rb.w, D);
+        scatter(accw, rb.x, rb.y, rb.z, rb.w, D);
+    }
+    const double RT = R_GAS * T;
+#pragma unroll 1
+    for (int r = gl; r < nrs; r += GL) {                               // surface reactions (production())
+        const uint32_t* rec = tb.sx + SX_WORDS * r;
+        const int nc = si_ncov(rec[4]);
+        const double* xe = tb.sxe + SXE_DOUBLES * r;
+        double k = skd[r] * xe[4];
+        if (nc) {
+            double s = 0.0;
+            for (int j = 0; j < 4; ++j) if (j < nc) s += xe[j] * conc[sp8(rec[5], j)];
+            k *= exp(-s / RT);
+        }
+        const double P = ((conc[sp8(rec[0], 0)] * conc[sp8(rec[0], 1)]) * (conc[sp8(rec[0], 2)] * conc[sp8(rec[0], 3)])) *
+                         (conc[sp8(rec[1], 0)] * conc[sp8(rec[1], 1)]);
+        scatter(accs, rec[6], rec[7], rec[8], rec[9], k * P);
     }
     wave_sync();
-    const double w = acc[gl];
+    const double w = gl < n ? accw[gl] : 0.0;
+    if (nrs == 0) {                                                    // gas only (:363-370)
+        wave_sync();
+        if (gl == 0) *p_out = p;
+        return gl < n ? w * Mk : 0.0;
+    }
+    const double sf = gl < n ? accs[gl] : 0.0;
     wave_sync();
     if (gl == 0) *p_out = p;
-    return gl < n ? w * Mk : 0.0;                                    // :363-370 (gas only)
+    if (gas) return (sf * Asv + w) * Mk;                               // :345, :363-370
+    if (gl < n) return sf * Asv_th * tb.sigma[gl] / MF(G);             // :367 / :370
+    return 0.0;
 }
 
-// Analytic Jacobian d(du)/du of a gas-only group, row gl per lane (jr[j] = J[gl][j]), at the state
-// of the RHS just evaluated (its concentrations and third-body sums are still in the species
-// block): J[k][j] = M_k / M_j * sum_r nu_kr dq_r/dc_j (same terms as the wavefront engine and the
-// oracle's jac_tc: mass-action partial products, third-body / falloff d[M] columns; the M_k / M_j
-// factor applied once per entry). Reactions in a uniform loop (every group evaluates reaction r
-// for its own state); the sparse partials go to their column through a scalar switch.
-template <int NM>
-__device__ __forceinline__ void q_jac(const Tab& tb, const double* sp, const double* kd, const double* fod, int gl,
+// Analytic Jacobian d(du)/du of a gas-only group's reactor, row gl per lane (jr[j] = J[gl][j]), at
+// the state of the RHS just evaluated (its concentrations and third-body sums are still in the
+// species block). The same terms as the wavefront engine's jacobian() and the oracle's jac_tc:
+// J[k][j] = M_k / M_j sum_r nu_kr dq_r/dc_j (mass-action partial products, third-body / falloff d[M]
+// columns; the M_k / M_j factor applied once per entry). Reactions in a uniform loop (every group
+// evaluates reaction r for its own state); the sparse partials reach their column through scalar
+// compares on the uniform species.
+template <int GL, int NM>
+__device__ __forceinline__ void g_jac(const Tab& tb, const double* sp, const double* kd, const double* fod, int gl,
                                       double (&jr)[NM]) {
-    const int n = MF(n), nrg = MF(nrg);
+    typedef grp::GLay<GL> L;
+    const int n = MF(n), ng = MF(ng), nrg = MF(nrg);
     const bool xm = (MF(conv) & 2) != 0;
 #pragma unroll
     for (int j = 0; j < NM; ++j) jr[j] = 0.0;
     const unsigned gl8 = (unsigned)gl * 8u;
-#pragma unroll 1
-    for (int r = 0; r < nrg; ++r) {
-        const auto rr = rx_rec(tb.rx, r);
-        const uint32_t w0 = uni((int)rr[0]), w1 = uni((int)rr[1]), info = uni((int)rr[2]);
-        const uint32_t s0 = uni((int)rr[4]), s1 = uni((int)rr[5]), s2 = uni((int)rr[6]), s3 = uni((int)rr[7]);
-        double cf[4], cb[4];
-        const double D = q_mass_action(sp, kd, w0, w1, r, cf, cb);
-        double pre = 1.0, coefM = 0.0;
-        const int tbk = gi_tb(info);
-        if (tbk) {
-            const double Mc = sp[quad::SP_MC + gi_tbidx(info)];
-            if (tbk == 1) { pre = Mc; coefM = 1.0; }
-            else {
-                double fac, dfac;
-                falloff<true>(fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
-                const double xs = xm ? Mc * 1e-6 : 1.0;             // [M] in mol/cm3 (reference)
-                pre = fac * xs;
-                coefM = dfac * xs + (xm ? fac * 1e-6 : 0.0);
-            }
-        }
-        // this row's net stoichiometric coefficient in reaction r
+    // this row's net stoichiometric coefficient from a reaction's scatter list
+    auto row_nu = [&](uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
         const int cnt = (int)(s3 >> 24);
         const uint32_t sw[3] = {s0, s1, s2};
         double nu = 0.0;
 #pragma unroll
         for (int e = 0; e < 6; ++e)
             if (e < cnt && sl_off(sw[e >> 1], e & 1) == gl8) nu += (double)sl_nu(s3, e);
-        // third-body / falloff: d q / d c_j = D coefM eff_j (all gas species)
-        if (gi_tb(info)) {
+        return nu;
+    };
+#pragma unroll 1
+    for (int r = 0; r < nrg; ++r) {
+        const auto rr = rx_rec(tb.rx, r);
+        const uint32_t w0 = uni((int)rr[0]), w1 = uni((int)rr[1]), info = uni((int)rr[2]);
+        const uint32_t s0 = uni((int)rr[4]), s1 = uni((int)rr[5]), s2 = uni((int)rr[6]), s3 = uni((int)rr[7]);
+        double cf[4], cb[4];
+        const double D = g_mass_action<GL>(sp, kd, w0, w1, r, cf, cb);
+        double pre = 1.0, coefM = 0.0;
+        const int tbk = gi_tb(info);
+        if (tbk) {
+            const double Mc = sp[L::MC + gi_tbidx(info)];
+            if (tbk == 1) { pre = Mc; coefM = 1.0; }
+            else {
+                double fac, dfac;
+                falloff<true>(fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
+                const double xs = xm ? Mc * 1e-6 : 1.0;               // [M] in mol/cm3 (reference)
+                pre = fac * xs;
+                coefM = dfac * xs + (xm ? fac * 1e-6 : 0.0);
+            }
+        }
+        const double nu = row_nu(s0, s1, s2, s3);
+        if (tbk) {                                                     // d q / d c_j = D coefM eff_j
             const double dm = nu * D * coefM;
             const double* eff = MF(tb_eff) + (size_t)gi_tbidx(info) * MF(n);
 #pragma unroll
-            for (int j = 0; j < NM; ++j) if (j < n) jr[j] = fma(dm, eff[j], jr[j]);
+            for (int j = 0; j < NM; ++j) if (j < ng) jr[j] = fma(dm, eff[j], jr[j]);
         }
-        // mass-action partials: slot e of the forward (backward) product
         const double kf = kd[2 * r], kr = kd[2 * r + 1];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; ++e) {                                  // slot e of the forward (backward) product
             double pf = kf * pre, pb = -kr * pre;
 #pragma unroll
             for (int e2 = 0; e2 < 4; ++e2)
@@ -247,48 +339,161 @@ __device__ __forceinline__ void q_jac(const Tab& tb, const double* sp, const dou
     }
     const double Mk = tb.molwt[gl];
 #pragma unroll
-    for (int j = 0; j < NM; ++j) jr[j] = (gl < n && j < n) ? jr[j] * (Mk / tb.molwt[j]) : 0.0;
+    for (int j = 0; j < NM; ++j) jr[j] = (gl < ng && j < ng) ? jr[j] * (Mk / tb.molwt[j]) : 0.0;
+#pragma unroll
+    for (int j = 0; j < NM; ++j) if (!(gl < n && j < n)) jr[j] = 0.0;
 }
 
-// compile-time loop: f(std::integral_constant<int, K>) for K = B .. E-1
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        sfor<B + 1, E>(f);
+// Analytic Jacobian of a group's reactor with surface chemistry, in column passes as the wavefront
+// engine's general jacobian() (brhip_device.hpp; oracle jac_tc): for each component j, the reactions
+// whose rate depends on j (host column lists) spread over the group's lanes compute dq_r/du_j and
+// scatter nu_kr dq_r/du_j into the production sums (gas reactions: d/dc_j, M_k / M_j applied per
+// row; surface reactions: reactant partials with dc/du = 1/M, 1 (sticking) or Gamma/sigma and the
+// coverage-dependent activation term -eps/RT q), then lane k writes J[k][j] = M_k w / M_j + M_k Asv
+// s (gas rows) or Asv_th sigma_k / Gamma s (surface rows) to the saved-J slot through `jst`. No
+// register tile: the state it needs is the species block of the RHS just evaluated.
+template <int GL, class JST>
+__device__ __forceinline__ void g_jac_cols(const Tab& tb, double* sp, const double* kd, const double* fod, const double* skd,
+                                           double T, double Asv, double Asv_th, int gl, JST&& jst) {
+    typedef grp::GLay<GL> L;
+    const int n = MF(n), ng = MF(ng), nrg = MF(nrg);
+    const bool xm = (MF(conv) & 2) != 0;
+    const double RT = R_GAS * T, Gs = MF(G);
+    const double* conc = sp + L::CONC;
+    double* accw = sp + L::ACCW;
+    double* accs = sp + L::ACCS;
+    const double Mk = tb.molwt[gl];
+    const int* cp = MF(col_ptr);
+    const int* cr = MF(col_rx);
+#pragma unroll 1
+    for (int j = 0; j < n; ++j) {
+        accw[gl] = 0.0;
+        accs[gl] = 0.0;
+        wave_sync();
+        const int cb = cp[j], ce = cp[j + 1];
+#pragma unroll 1
+        for (int i = cb + gl; i < ce; i += GL) {
+            const int rr = cr[i];
+            if (rr < nrg) {                                              // gas reaction: dq/dc_j
+                const int r = rr;
+                const auto rec = rx_rec(tb.rx, r);
+                const uint32_t info = rec[2];
+                const int nf = gi_nf(info), nr = gi_nr(info), tbk = gi_tb(info);
+                double cf[4], cb4[4];
+                const double D = g_mass_action<GL>(sp, kd, rec[0], rec[1], r, cf, cb4);
+                double pre = 1.0, coefM = 0.0;
+                if (tbk) {
+                    const double Mc = sp[L::MC + gi_tbidx(info)];
+                    if (tbk == 1) { pre = Mc; coefM = 1.0; }
+                    else {
+                        double fac, dfac;
+                        falloff<true>(fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
+                        pre = fac * (xm ? Mc * 1e-6 : 1.0);
+                        coefM = dfac * (xm ? Mc * 1e-6 : 1.0) + (xm ? fac * 1e-6 : 0.0);
+                    }
+                }
+                double d = 0.0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) if (e < nf && sp8(rec[0], e) == j) {
+                    double pr = kd[2 * r];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nf) pr *= conc[sp8(rec[0], e2)];
+                    d += pre * pr;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) if (e < nr && sp8(rec[1], e) == j) {
+                    double pr = kd[2 * r + 1];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) if (e2 != e && e2 < nr) pr *= conc[sp8(rec[1], e2)];
+                    d -= pre * pr;
+                }
+                if (tbk && j < ng) d += (D * coefM) * MF(tb_eff)[gi_tbidx(info) * n + j];
+                scatter(accw, rec[4], rec[5], rec[6], rec[7], d);
+            } else {                                                     // surface reaction: dq/du_j
+                const int r = rr - nrg;
+                const uint32_t* rec = tb.sx + SX_WORDS * r;
+                const uint32_t info = rec[4];
+                const int nf = si_nf(info), nc = si_ncov(info);
+                const bool stick = si_stick(info);
+                const double* eps = tb.sxe + SXE_DOUBLES * r;
+                double k = skd[r];
+                if (nc) {
+                    double s = 0.0;
+                    for (int jj = 0; jj < 4; ++jj) if (jj < nc) s += eps[jj] * conc[sp8(rec[5], jj)];
+                    k *= exp(-s / RT);
+                }
+                double cv[6], dc[6];
+                int spe[6];
+#pragma unroll
+                for (int e = 0; e < 6; ++e) {
+                    spe[e] = e < nf ? (e < 4 ? sp8(rec[0], e) : sp8(rec[1], e - 4)) : -1;
+                    cv[e] = 1.0; dc[e] = 0.0;
+                    if (e < nf) {
+                        const int s = spe[e];
+                        if (s < ng) { cv[e] = conc[s]; dc[e] = 1.0 / tb.molwt[s]; }
+                        else if (stick) { cv[e] = conc[s]; dc[e] = 1.0; }
+                        else { cv[e] = conc[s] * Gs / tb.sigma[s]; dc[e] = Gs / tb.sigma[s]; }
+                    }
+                }
+                double d = 0.0;
+#pragma unroll
+                for (int e = 0; e < 6; ++e) if (spe[e] == j) {
+                    double pr = k;
+#pragma unroll
+                    for (int e2 = 0; e2 < 6; ++e2) if (e2 != e && e2 < nf) pr *= cv[e2];
+                    d += pr * dc[e];
+                }
+                if (nc) {
+                    double P = 1.0;
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) if (e < nf) P *= cv[e];
+                    const double q = k * P;
+                    for (int jj = 0; jj < 4; ++jj) if (jj < nc && (int)sp8(rec[5], jj) == j) d += q * (-eps[jj] / RT);
+                }
+                scatter(accs, rec[6], rec[7], rec[8], rec[9], d);
+            }
+        }
+        wave_sync();
+        const bool act = gl < n;
+        const double w = act ? accw[gl] : 0.0;
+        const double sf = act ? accs[gl] : 0.0;
+        double v;
+        if (gl < ng) v = (j < ng ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * sf;
+        else v = Asv_th * tb.sigma[gl] / Gs * sf;
+        jst(j, act ? v : 0.0);
+        wave_sync();
     }
 }
-// value of lane K of this lane's 16-lane row (DPP row_newbcast: a VALU move, no LDS crossbar)
-template <int K>
-__device__ __forceinline__ double row_bcast(double v) { return dppd<0x150 + K>(v); }
 
 // group pivot of step k: the first max |a| (bit patterns: a 32-bit max over the high words, then
-// over the low words, then the lowest lane) among candidate lanes of the row; returns that lane
+// over the low words, then the lowest lane) among candidate lanes of the group; returns that lane
 // within the group. SUNDIALS denseGETRF takes the first row of largest |a_ik| in the current
 // (already interchanged) row order -- the lane order here.
-__device__ __forceinline__ int q_pivot(double a, bool cand, int gl) {
+template <int GL>
+__device__ __forceinline__ int g_pivot(double a, bool cand, int gl) {
     const unsigned long long bits = (unsigned long long)__double_as_longlong(a) & 0x7fffffffffffffffull;
     const unsigned hi = cand ? (unsigned)(bits >> 32) : 0u;
-    const unsigned mh = row_umax(hi);
+    const unsigned mh = group_umax<GL>(hi);
     const bool top = cand && hi == mh;
     const unsigned lo = top ? (unsigned)bits : 0u;
-    const unsigned ml = row_umax(lo);
+    const unsigned ml = group_umax<GL>(lo);
     const bool top2 = top && lo == ml;
     const unsigned key = top2 ? ~(unsigned)gl : 0u;
-    return (int)(~row_umax(key));
+    return (int)(~group_umax<GL>(key));
 }
 
 // LU of A = I - gamma J with partial pivoting as SUNDIALS denseGETRF (src/BatchReactor.jl:204-210:
 // CVODE's dense linear solver), one row per lane in registers, rows interchanged physically (lane
 // = current row position): after the factorization lane s holds row s of the factors (L's
 // multipliers in a[k < s], U in a[k >= s]), dinv = 1 / u_ss, and orig = the original row now at
-// lane s (the accumulated interchanges, applied to b by q_solve). Interchanges are bpermutes of the
+// lane s (the accumulated interchanges, applied to b by g_solve). Interchanges are bpermutes of the
 // two rows' registers, issued only when some group of the wave needs one; the pivot row's values
-// reach the row by DPP row broadcasts. Returns 0 or k+1 (zero pivot at step k, as denseGETRF).
-template <int NM>
-__device__ __forceinline__ int q_lu(const double (&jr)[NM], double gamma, int n, int gl, double (&a)[NM], int& orig,
+// reach the group by DPP broadcasts from the compile-time lane k. Returns 0 or k+1 (zero pivot at
+// step k, as denseGETRF).
+template <int GL, int NM>
+__device__ __forceinline__ int g_lu(const double (&jr)[NM], double gamma, int n, int gl, double (&a)[NM], int& orig,
                                     double& dinv) {
-    const int gb = (int)(threadIdx.x & 48);
+    const int gb = (int)(threadIdx.x & (64 - GL));
 #pragma unroll
     for (int j = 0; j < NM; ++j) a[j] = ((j == gl && gl < n) ? 1.0 : 0.0) - gamma * jr[j];
     orig = gl;
@@ -297,56 +502,56 @@ __device__ __forceinline__ int q_lu(const double (&jr)[NM], double gamma, int n,
     sfor<0, NM>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         if (k < n) {
-            const int p = q_pivot(a[k], gl >= k && gl < n, gl);
-            if (__ballot(p != k) != 0) {                           // interchange rows k and p
+            const int p = g_pivot<GL>(a[k], gl >= k && gl < n, gl);
+            if (__ballot(p != k) != 0) {                                 // interchange rows k and p
                 const int src = gb + (gl == k ? p : (gl == p ? k : gl));
 #pragma unroll
                 for (int j = 0; j < NM; ++j) a[j] = lane_pull(a[j], src);
                 orig = __builtin_amdgcn_ds_bpermute(src * 4, orig);
             }
-            const double pv = row_bcast<k>(a[k]);
+            const double pv = group_bcast<GL, k>(a[k]);
             if (pv == 0.0 && fail == 0) fail = k + 1;
             const double rinv = 1.0 / pv;
             const bool below = gl > k;
-            const double l = below ? a[k] * rinv : 0.0;                // denseGETRF: a_ik *= 1 / a_kk
+            const double l = below ? a[k] * rinv : 0.0;                  // denseGETRF: a_ik *= 1 / a_kk
             if (below) a[k] = l;
             if (gl == k) dinv = rinv;
 #pragma unroll
             for (int j = k + 1; j < NM; ++j)
-                if (j < n) a[j] = fma(-row_bcast<k>(a[j]), l, a[j]);
+                if (j < n) a[j] = fma(-group_bcast<GL, k>(a[j]), l, a[j]);
         }
     });
     return fail;
 }
 
-// solve (I - gamma J) x = b with q_lu's factors (denseGETRS): b interchanged (P b: one bpermute),
-// forward with the unit L, backward with U; each step's pivot value reaches the row by a DPP
+// solve (I - gamma J) x = b with g_lu's factors (denseGETRS): b interchanged (P b: one bpermute),
+// forward with the unit L, backward with U; each step's pivot value reaches the group by a DPP
 // broadcast from the compile-time lane k. b and x in component order (lane gl).
-template <int NM>
-__device__ __forceinline__ double q_solve(const double (&a)[NM], int orig, double dinv, int n, int gl, double b) {
-    const int gb = (int)(threadIdx.x & 48);
+template <int GL, int NM>
+__device__ __forceinline__ double g_solve(const double (&a)[NM], int orig, double dinv, int n, int gl, double b) {
+    const int gb = (int)(threadIdx.x & (64 - GL));
     double y = lane_pull(gl < n ? b : 0.0, gb + orig);
-    sfor<0, NM>([&](auto kc) {                                        // L y = P b
+    sfor<0, NM>([&](auto kc) {                                          // L y = P b
         constexpr int k = decltype(kc)::value;
         if (k + 1 < n) {
-            const double yk = row_bcast<k>(y);
+            const double yk = group_bcast<GL, k>(y);
             y = fma(-((gl > k) ? a[k] : 0.0), yk, y);
         }
     });
     double x = 0.0;
-    sfor<0, NM>([&](auto kc) {                                        // U x = y, k = n-1 .. 0
+    sfor<0, NM>([&](auto kc) {                                          // U x = y, k = n-1 .. 0
         constexpr int k = NM - 1 - decltype(kc)::value;
         if (k < n) {
             if (gl == k) x = y * dinv;
-            const double xk = row_bcast<k>(x);
+            const double xk = group_bcast<GL, k>(x);
             y = fma(-((gl < k) ? a[k] : 0.0), xk, y);
         }
     });
     return gl < n ? x : 0.0;
 }
 
-// the controller entry points for 16-lane groups (BR_QCTL_NOINLINE: out of line, so their register
-// allocation is separate from the hot loop's)
+// the controller entry points for GL-lane groups (BR_QCTL_NOINLINE: out of line, so their register
+// allocation is separate from the hot loop's; measured: more VGPRs, kept inline)
 #ifndef BR_QCTL_NOINLINE
 #define BR_QCTL_NOINLINE 0
 #endif
@@ -355,49 +560,66 @@ __device__ __forceinline__ double q_solve(const double (&a)[NM], int orig, doubl
 #else
 #define BR_QCTL_ATTR __forceinline__
 #endif
-__device__ BR_QCTL_ATTR int q_post_rhs(LCtl* C, VT<1, 16>& V, int gl, const double (&f)[1], double (&b)[1]) {
-    return ctl_post_rhs<1, 16>(C, V, gl, f, b);
+template <int GL>
+__device__ BR_QCTL_ATTR int g_post_rhs(LCtl* C, VT<1, GL>& V, int gl, const double (&f)[1], double (&b)[1]) {
+    return ctl_post_rhs<1, GL>(C, V, gl, f, b);
 }
-__device__ BR_QCTL_ATTR int q_post_solve(LCtl* C, VT<1, 16>& V, int gl, double (&delta)[1], int lu_fail) {
-    return ctl_post_solve<1, 16>(C, V, gl, delta, lu_fail);
+template <int GL>
+__device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VT<1, GL>& V, int gl, double (&delta)[1], int lu_fail) {
+    return ctl_post_solve<1, GL>(C, V, gl, delta, lu_fail);
 }
 
 #ifndef BR_QWPB
-#define BR_QWPB 4   // waves per workgroup (16 reactors); tables staged once per workgroup
+#define BR_QWPB 4   // waves per workgroup (16 quad / 8 pair reactors); tables staged once per workgroup
 #endif
 #ifndef BR_QWPE
-#define BR_QWPE 3   // waves per SIMD the register allocation targets (<= 168 VGPRs)
+#define BR_QWPE 3   // waves per SIMD the register allocation targets for 16-lane groups (<= 168 VGPRs;
+                    // quad H2/O2: 882k reactors/s at 3 vs 693k at 2, round 4)
+#endif
+#ifndef BR_QWPE32
+#define BR_QWPE32 3 // ... for 32-lane groups (surface-only Ni/CH4, n = 20: 194.8k reactors/s at 3 (228 B/lane
+                    // spilled) vs 159.1k at 2; the wavefront engine does 217.7k, round 4)
 #endif
 
-// the quad integrator kernel: persistent grid, every group takes reactor indices from o.work
-template <int NM>
-__global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR_QWPE))) void k_quad(DevMech M, int N, const double* __restrict__ Tv,
-                                                        double* __restrict__ U, const double* __restrict__ tfv, KOpts o,
-                                                        double* __restrict__ stats, double* __restrict__ Jws) {
+// the group integrator kernel: persistent grid, every group takes reactor indices from o.work
+template <int GL, int NM>
+__global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL == 16 ? BR_QWPE : BR_QWPE32))) void k_group(
+    DevMech M, int N, const double* __restrict__ Tv, const double* __restrict__ Asvv, double* __restrict__ U,
+    const double* __restrict__ tfv, KOpts o, double* __restrict__ stats, double* __restrict__ Jws) {
+    static_assert(NM <= GL, "register tile wider than the group");
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     stage_tables(M, smem_raw);
     const Tab tb = tab_view<1>(smem_raw, M);
-    const int lane = threadIdx.x & 63, gl = lane & 15;
-    const int grp = (int)(threadIdx.x >> 4);                          // group within the workgroup
-    const int slot = blockIdx.x * (BR_QWPB * 4) + grp;                // workspace slot of this group
-    const int RB = quad::block_bytes(MF(nrg), MF(nfo));
+    constexpr int GPW = 64 / GL;                                        // groups per wave
+    const int lane = threadIdx.x & 63, gl = lane & (GL - 1);
+    const int grp = (int)(threadIdx.x / GL);                            // group within the workgroup
+    const int slot = blockIdx.x * (BR_QWPB * GPW) + grp;                // workspace slot of this group
+    const int RB = grp::block_bytes(GL, MF(nrg), MF(nfo), MF(nrs));
     char* rbase = smem_raw + M.img_bytes + (size_t)grp * RB;
     LCtl* C = (LCtl*)rbase;
-    VA<1, quad::G> V{(LDbl*)(rbase + CTL_BYTES), gl};
-    double* sp = reinterpret_cast<double*>(rbase + CTL_BYTES + quad::vbytes());
-    double* kd = reinterpret_cast<double*>(rbase + quad::kd_off());
+    VA<1, GL> V{(LDbl*)(rbase + CTL_BYTES), gl};
+    double* sp = reinterpret_cast<double*>(rbase + grp::sp_off(GL));
+    double* kd = reinterpret_cast<double*>(rbase + grp::kd_off(GL));
     double* fod = kd + 2 * MF(nrg);
-    BR_GLOBAL double* Jq = launder(Jws) + (size_t)slot * (quad::G * quad::G);
+    double* skd = fod + 4 * MF(nfo);
+    // the group's saved-J slot through a buffer resource: lane offset in a VGPR, the column offset
+    // j GL 8 as the instruction's scalar offset (as 64-bit addresses, the columns past 4 KB of a 32-lane
+    // slot were materialised per column, hoisted out of the loop and spilled)
+    const __amdgpu_buffer_rsrc_t jrs = __builtin_amdgcn_make_buffer_rsrc((void*)launder(Jws), (short)0, 0x7fffffff, 0x00020000);
+    const unsigned jvo = (unsigned)(slot * GL * GL + gl) * 8u;
+    auto jst = [&](int j, double v) { __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), jrs, jvo, j * (GL * 8), 0); };
+    auto jld = [&](int j) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(jrs, jvo, j * (GL * 8), 0)); };
     const int n = MF(n);
-    double* p_last = reinterpret_cast<double*>(rbase);                // Ctl::p_last is the first field
+    const bool asv_fixed = (MF(conv) & 4) != 0;
+    double* p_last = reinterpret_cast<double*>(rbase);                  // Ctl::p_last is the first field
     // this group's reactor: the first one from the work counter
     auto take = [&]() -> int {
         int v = 0;
         if (gl == 0) v = atomicAdd(o.work, 1);
-        return __builtin_amdgcn_ds_bpermute((int)(threadIdx.x & 48) * 4, v);
+        return __builtin_amdgcn_ds_bpermute((int)(threadIdx.x & (64 - GL)) * 4, v);
     };
     int rid = take();
-    double T = 0.0;
+    double T = 0.0, Asv = 1.0, Asv_th = 1.0;
     bool fresh = true;
     int dqj = -1;   // >= 0: building column dqj of the DQ Jacobian
     double a[NM];
@@ -417,7 +639,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
     for (;;) {
         if (__ballot(rid < N) == 0) break;
         if (rid < N) {
-            if (fresh) {                                              // ---- CVodeInit for reactor rid
+            if (fresh) {                                                // ---- CVodeInit for reactor rid
                 fresh = false;
                 cyc0 = wall_clock64();
 #if BR_PHASE_CLOCKS
@@ -425,10 +647,12 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
                 q_all = clock64();
 #endif
                 T = Tv[rid];
+                Asv = Asvv ? Asvv[rid] : 1.0;
+                Asv_th = asv_fixed ? 1.0 : Asv;
                 C->a_rtol = o.rtol; C->a_atol = o.atol; C->a_hmax_inv = o.hmax_inv; C->a_ufac = o.ufac;
                 C->a_max_steps = o.max_steps; C->a_trace_cap = 0; C->a_trace = nullptr; C->a_rid = rid; C->a_n = n;
                 C->a_ign = o.ign; C->a_nout = o.nout; C->a_tout = o.tout; C->a_yout = o.yout;
-                q_init_tconst<NM>(tb, sp, kd, fod, T, gl);
+                g_init_tconst<GL>(tb, sp, kd, fod, skd, T, gl);
                 const bool act = gl < n;
                 const double u0 = act ? U[(size_t)rid * n + gl] : 0.0;
 #pragma unroll
@@ -436,7 +660,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
                 V.at(0, 0) = u0;
                 V.at(V_Y, 0) = u0;
                 V.at(V_EWT, 0) = act ? 1.0 / (o.rtol * fabs(u0) + o.atol) : 1.0;
-                const double su = row_sum(act ? fabs(u0) : 0.0);
+                const double su = gsum<GL>(act ? fabs(u0) : 0.0);
 #pragma unroll
                 for (int i = 0; i < QMAX + 2; ++i) C->tau[i] = 0.0;
 #pragma unroll
@@ -457,9 +681,9 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
                 C->dq_mininc = 1.0; C->nfe_dq = 0;
                 if (o.ign >= 0) {
                     double uv[1] = {u0};
-                    C->ign_x = mole_frac_of<1, quad::G>(uv, gl, o.ign);
+                    C->ign_x = mole_frac_of<1, GL>(uv, gl, o.ign);
                 }
-                if (o.nout) {                                         // outputs at t <= 0: the initial state
+                if (o.nout) {                                           // outputs at t <= 0: the initial state
                     int io = 0;
                     while (io < o.nout && !(o.tout[io] > 0.0)) {
                         if (act) o.yout[((size_t)rid * o.nout + io) * n + gl] = u0;
@@ -471,15 +695,15 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
             }
             // ---- one RHS for this group's reactor, then its controller. dqj >= 0: this RHS is at
             // y + inc_dqj e_dqj, column dqj of CVODE's DQ Jacobian (cvLsDenseDQJac, k_integrate's
-            // dq_* steps with 16-lane groups)
+            // dq_* steps with GL-lane groups)
             double yv = V.at(V_Y, 0);
             if (dqj >= 0) {
                 double inc[1];
-                dq_incs<1, quad::G>(C, V, gl, inc);
+                dq_incs<1, GL>(C, V, gl, inc);
                 if (gl == dqj) yv += inc[0];
             }
             QCLK(c_r);
-            const double fv = q_rhs<NM>(tb, sp, kd, fod, T, yv, gl, p_last);
+            const double fv = g_rhs<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, yv, gl, p_last);
             QACC(q_rhs_c, c_r);
             double f[1] = {fv}, b[1];
             int act_code;
@@ -487,22 +711,23 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
             QCLK(c_c);
             if (dqj >= 0) {
                 double inc[1];
-                dq_incs<1, quad::G>(C, V, gl, inc);
-                const double ii = 1.0 / gbcast<quad::G>(inc[0], dqj);
-                Jq[dqj * quad::G + gl] = ii * fv - ii * V.at(V_TEMP, 0);
+                dq_incs<1, GL>(C, V, gl, inc);
+                const double ii = 1.0 / gbcast<GL>(inc[0], dqj);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ii * fv - ii * V.at(V_TEMP, 0)), jrs,
+                                                      jvo + (unsigned)dqj * (GL * 8u), 0, 0);
                 C->nfe_dq = C->nfe_dq + 1;
                 if (++dqj < n) {
                     act_code = A_RHS;
                 } else {
                     dqj = -1;
-                    dq_newton_rhs<1, quad::G>(C, V, gl, b);
+                    dq_newton_rhs<1, GL>(C, V, gl, b);
                     act_code = A_SETUP;
                     jac_ready = true;
                 }
             } else {
-                act_code = q_post_rhs(C, V, gl, f, b);
+                act_code = g_post_rhs<GL>(C, V, gl, f, b);
                 if (act_code == A_SETUP && o.dq_jac && C->newj) {
-                    dq_begin<1, quad::G>(C, V, gl, f);
+                    dq_begin<1, GL>(C, V, gl, f);
                     dqj = 0;
                     act_code = A_RHS;
                 }
@@ -510,31 +735,37 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
             QACC(q_ctl_c, c_c);
             int lu_fail = 0;
             if (act_code == A_SETUP) {
-                if (!jac_ready && C->newj) {                          // analytic Jacobian at y, saved
+                if (!jac_ready && C->newj) {                            // analytic Jacobian at y, saved
                     QCLK(c_j);
-                    double jr[NM];
-                    q_jac<NM>(tb, sp, kd, fod, gl, jr);
+                    if (MF(nrs) == 0) {                                 // gas only: register rows
+                        double jr[NM];
+                        g_jac<GL, NM>(tb, sp, kd, fod, gl, jr);
 #pragma unroll
-                    for (int j = 0; j < NM; ++j) Jq[j * quad::G + gl] = jr[j];
+                        for (int j = 0; j < NM; ++j) jst(j, jr[j]);
+                    } else {                                            // surface chemistry: column passes
+                        g_jac_cols<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, gl, jst);
+#pragma unroll 1
+                        for (int j = n; j < NM; ++j) jst(j, 0.0);             // padding columns
+                    }
                     QACC(q_jac_c, c_j);
                 }
                 QCLK(c_l);
                 double jr[NM];
 #pragma unroll
-                for (int j = 0; j < NM; ++j) jr[j] = Jq[j * quad::G + gl];
-                lu_fail = q_lu<NM>(jr, C->gamma, n, gl, a, orig, dinv);
+                for (int j = 0; j < NM; ++j) jr[j] = jld(j);
+                lu_fail = g_lu<GL, NM>(jr, C->gamma, n, gl, a, orig, dinv);
                 QACC(q_lu_c, c_l);
             }
             if (act_code == A_SOLVE || act_code == A_SETUP) {
                 QCLK(c_s);
                 double delta[1] = {0.0};
-                if (!lu_fail) delta[0] = q_solve<NM>(a, orig, dinv, n, gl, b[0]);
+                if (!lu_fail) delta[0] = g_solve<GL, NM>(a, orig, dinv, n, gl, b[0]);
                 QACC(q_sol_c, c_s);
                 QCLK(c_p);
-                act_code = q_post_solve(C, V, gl, delta, lu_fail);
+                act_code = g_post_solve<GL>(C, V, gl, delta, lu_fail);
                 QACC(q_ctl_c, c_p);
             }
-            if (act_code == A_DONE) {                                 // ---- results, next reactor
+            if (act_code == A_DONE) {                                   // ---- results, next reactor
                 const int status = C->status;
                 const double u_out = status ? V.at(0, 0) : V.at(V_Y, 0);
                 if (gl < n) U[(size_t)rid * n + gl] = u_out;
@@ -558,4 +789,6 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(BR
             }
         }
     }
+#undef QCLK
+#undef QACC
 }

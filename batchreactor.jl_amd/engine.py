@@ -61,14 +61,18 @@ class Engine:
     def kernel_name(self) -> str:
         """the integrator kernel br_integrate_dev launches for this mechanism"""
         nm = _lib.lib().br_mech_engine(self.h)
-        return f"k_lane<{nm}>" if nm > 0 else f"k_quad<{-nm}>" if nm < 0 else f"k_integrate<{self.nmax}>"
+        if nm < 0:   # group engine: -(100 * group width + register width)
+            return f"k_group<{-nm // 100}, {-nm % 100}>"
+        return f"k_lane<{nm}>" if nm > 0 else f"k_integrate<{self.nmax}>"
 
     @property
     def engine(self) -> str:
-        """'lane' (one reactor per lane), 'quad' (four reactors per wavefront, one per 16-lane row;
-        both for small gas mechanisms) or 'wave' (one reactor per wavefront)"""
+        """'lane' (one reactor per lane, small gas mechanisms), 'quad' / 'pair' (four / two reactors
+        per wavefront, one per 16- / 32-lane group, n <= 16 / 32) or 'wave' (one reactor per wavefront)"""
         nm = _lib.lib().br_mech_engine(self.h)
-        return "lane" if nm > 0 else "quad" if nm < 0 else "wave"
+        if nm < 0:
+            return "quad" if -nm // 100 == 16 else "pair"
+        return "lane" if nm > 0 else "wave"
 
     @property
     def launch_info(self) -> dict:

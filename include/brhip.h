@@ -173,12 +173,14 @@ typedef struct br_batch_input {
 int br_read_batch_xml(const char* path, br_batch_input* out);
 int br_mech_destroy(br_mech* m);
 int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs);
-/* integrator engine br_integrate* uses for this mechanism: 0 = one reactor per
- * wavefront (k_integrate), NM > 0 = one reactor per lane with NM-wide register tiles (k_lane,
- * gas-only mechanisms with n <= 12), -NM < 0 = four reactors per wavefront, one per 16-lane row
- * (k_quad, gas-only mechanisms with n <= 16 and <= 32 third-body efficiency sets). All three take
- * br_opts.dq_jacobian. Traced integrations always use the wavefront engine; env
- * BRHIP_ENGINE = wave | lane | quad forces one where the mechanism is eligible. */
+/* integrator engine br_integrate* uses for this mechanism: 0 = one reactor per wavefront
+ * (k_integrate), NM > 0 = one reactor per lane with NM-wide register tiles (k_lane, gas-only
+ * mechanisms with n <= 12), -(100 GL + NM) < 0 = a group engine, one reactor per GL-lane group of a
+ * wavefront with NM-wide register tiles (k_group<GL, NM>; GL = 16 "quad", n <= 16, the default for
+ * such mechanisms; GL = 32 "pair", 16 < n <= 32; gas and surface chemistry, <= 32 third-body
+ * efficiency sets). All of them take br_opts.dq_jacobian. Traced integrations always use the
+ * wavefront engine; env BRHIP_ENGINE = wave | lane | quad | pair forces one where the mechanism is
+ * eligible. */
 int br_mech_engine(const br_mech* m);
 /* launch geometry of the wavefront engine for this mechanism (diagnostics): reactors (waves) per
  * workgroup, resident waves per CU (occupancy calculator: VGPRs and LDS), LDS bytes per

@@ -10,7 +10,7 @@ for L in libs:
     tot = {}
     for f in glob.glob(f"gpurun_out/pmcab_{L}_*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if any(k in r["Kernel_Name"] for k in ("k_integrate", "k_lane", "k_quad")):
+            if any(k in r["Kernel_Name"] for k in ("k_integrate", "k_lane", "k_quad", "k_group")):
                 tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     pr = {k: v / n for k, v in tot.items()}
     if "FETCH_SIZE" in pr:   # kB -> bytes; x2 gfx950 streaming-read correction (MI355X_MICROARCH.md HBM)

@@ -16,7 +16,7 @@ import sys
 def total(path, name):
     s = 0.0
     for r in csv.DictReader(open(path)):
-        if any(k in r["Kernel_Name"] for k in ("k_integrate", "k_lane", "k_quad")) and r["Counter_Name"] == name:
+        if any(k in r["Kernel_Name"] for k in ("k_integrate", "k_lane", "k_quad", "k_group")) and r["Counter_Name"] == name:
             s += float(r["Counter_Value"])
     return s
 

@@ -658,7 +658,7 @@ def test_lane_and_wave_engines_agree(pkg, gpu, monkeypatch):
 
 
 def test_quad_engine_h2o2(pkg, orc, gpu, monkeypatch):
-    """Four-reactors-per-wave engine (k_quad: one reactor per 16-lane DPP row, the wavefront
+    """Four-reactors-per-wave engine (k_group<16, NM>, "quad": one reactor per 16-lane DPP row, the wavefront
     engine's CVODE controller instantiated for 16-lane groups, analytic Jacobian, LU in registers).
     N = 200 with ragged end times: groups take new reactors from the work counter while the other
     groups of their wave are mid-run. Tight tolerances: end states agree with the oracle to 1e-6
@@ -667,7 +667,7 @@ def test_quad_engine_h2o2(pkg, orc, gpu, monkeypatch):
     monkeypatch.setenv("BRHIP_ENGINE", "quad")
     pm, om = _mechs(pkg, orc, "h2o2")
     eng = pkg.Engine(pm)
-    assert eng.engine == "quad" and eng.kernel_name == "k_quad<9>"
+    assert eng.engine == "quad" and eng.kernel_name == "k_group<16, 9>"
     N = 200
     T, Asv, U0 = _ignition_inputs(pm, "h2o2", N, 6)
     tf = np.where(np.arange(N) % 3 == 0, 1e-3, 1e-2)            # ragged end times
@@ -697,7 +697,7 @@ def test_quad_engine_h2o2(pkg, orc, gpu, monkeypatch):
 
 
 def test_quad_engine_dq_jacobian(pkg, orc, gpu, monkeypatch):
-    """k_quad with CVODE's DQ Jacobian (br_opts.dq_jacobian, the reference's setting): n RHS per
+    """The quad engine with CVODE's DQ Jacobian (br_opts.dq_jacobian, the reference's setting): n RHS per
     Jacobian counted in nfe_dq, states at the 28 output times within the H2/O2-DQ bounds of
     test_integrate_parity against the oracle's cvLsDenseDQJac run, the same ignition time and step
     counts; tight tolerances: end states to 1e-6 relative."""
@@ -731,7 +731,7 @@ def test_quad_engine_dq_jacobian(pkg, orc, gpu, monkeypatch):
 
 
 def test_quad_engine_step_budget_and_wave_agreement(pkg, orc, gpu, monkeypatch):
-    """k_quad: max_steps = 60 stops every reactor that needs more with BR_ERR_MAXSTEPS (-1) after
+    """Quad engine: max_steps = 60 stops every reactor that needs more with BR_ERR_MAXSTEPS (-1) after
     exactly 60 steps, as the oracle's CVODE run; and the quad and wavefront engines (same
     controller, same analytic Jacobian) give the same end states at tight tolerances."""
     pm, om = _mechs(pkg, orc, "h2o2")
@@ -749,6 +749,51 @@ def test_quad_engine_step_budget_and_wave_agreement(pkg, orc, gpu, monkeypatch):
     Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
     assert np.all(sq["status"] == 0) and np.all(sw["status"] == 0)
     assert max(close_states(Uq[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(96)) <= 1.0
+
+
+def test_pair_engine_surface(pkg, orc, gpu, monkeypatch):
+    """Two-reactors-per-wave engine (k_group<32, 24>, "pair": one reactor per 32-lane half, surface
+    chemistry with coverage-dependent activation and sticking, the Asv quirk) on the surface-only
+    Ni/CH4 case (n = 20) against the oracle: the per-window bounds of test_integrate_parity at the 28
+    output times on a slice of the bench ensemble, step counts to 35 % / 3 %; tight tolerances with
+    per-reactor Asv in [1, 100]: end states to 1e-6 relative; the DQ Jacobian path: n RHS per Jacobian
+    and the same end states; and the same end states as the wavefront engine."""
+    monkeypatch.setenv("BRHIP_ENGINE", "pair")
+    from batchreactor_amd import ensemble
+    pm, om = _mechs(pkg, orc, "surf")
+    eng = pkg.Engine(pm)
+    assert eng.engine == "pair" and eng.kernel_name == "k_group<32, 24>", eng.kernel_name
+    N = 64
+    T, Asv, U0 = ensemble.make_inputs(pm, "surf", 0, N)
+    U, st = eng.integrate(T, Asv, U0, 10.0, tout=OUT_T)
+    assert np.all(st["status"] == 0), np.unique(st["status"])
+    bounds = BOUNDS[("surf", False)]
+    nst_o = 0
+    for i in range(N):
+        uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], 10.0, OUT_T, analytic_jac=True)
+        assert so["status"] == 0
+        eb = _band_errors(st["yout"][i], Yo, so["t_ign"])
+        for w, (bound, e) in enumerate(zip(bounds[:3], eb)):
+            assert e <= bound, (i, w, e, bound)
+        assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.35 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
+        nst_o += so["nsteps"]
+    assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
+    N = 48
+    T, Asv, U0 = _ignition_inputs(pm, "surf", N, 6)
+    for dq in (False, True):
+        U, st = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16, dq_jacobian=dq)
+        assert np.all(st["status"] == 0)
+        if dq:
+            assert np.all(st["nfe_dq"] == st["nje"] * pm.n)
+        for i in range(N):
+            uo, so, _ = om.integrate(T[i], Asv[i], U0[i], 1e-2, analytic_jac=not dq, rtol=1e-10, atol=1e-16)
+            assert so["status"] == 0
+            assert close_states(U[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, (dq, i)
+    Up, sp_ = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    monkeypatch.setenv("BRHIP_ENGINE", "wave")
+    Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    assert np.all(sw["status"] == 0)
+    assert max(close_states(Up[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(N)) <= 1.0
 
 
 def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
