@@ -107,8 +107,8 @@ typedef struct br_opts {
                                  left untouched                                             */
     int dq_jacobian;          /* 1: CVODE's dense difference-quotient Jacobian (cvLsDenseDQJac:
                                  the reference's CVODE_BDF() setting, src/BatchReactor.jl:140,
-                                 :204), n extra RHS per Jacobian, in both engines (lane and
-                                 wavefront); 0 (default): the analytic Jacobian              */
+                                 :204), n extra RHS per Jacobian, in every engine (lane,
+                                 group, wavefront); 0 (default): the analytic Jacobian       */
 } br_opts;
 
 #define BR_NSTAT 20

@@ -53,7 +53,7 @@ struct BrOpts
     nout::Cint
     tout::Ptr{Float64}          # [nout] ascending output times
     yout::Ptr{Float64}          # [N][nout][n]
-    dq_jacobian::Cint           # 1: CVODE's DQ Jacobian (cvLsDenseDQJac, the reference's setting), both engines
+    dq_jacobian::Cint           # 1: CVODE's DQ Jacobian (cvLsDenseDQJac, the reference's setting), every engine
 end
 BrOpts(; rtol=1e-6, atol=1e-10, max_steps=100_000, device=0, ignition_species=0) =
     BrOpts(rtol, atol, Cint(max_steps), Cint(device), 0.0, Cint(0), 0.0, Cint(ignition_species), Cint(0),
