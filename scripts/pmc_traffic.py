@@ -30,7 +30,7 @@ def main():
     res = {"reactors": n, "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
            "read_bytes_corrected": rd, "write_bytes": wr,
            "bytes_per_reactor": (rd + wr) / n,
-           "note": "FETCH_SIZE x2 (gfx950 correction), KiB->B; integrator dispatches (k_integrate / k_lane / k_quad) only"}
+           "note": "FETCH_SIZE x2 (gfx950 correction), KiB->B; integrator dispatches (k_integrate / k_lane / k_group) only"}
     if len(sys.argv) > 5:
         hit = total(sys.argv[5], "TCC_HIT_sum")
         miss = total(sys.argv[5], "TCC_MISS_sum")
