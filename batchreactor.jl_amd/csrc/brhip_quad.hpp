@@ -725,7 +725,9 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
                     jac_ready = true;
                 }
             } else {
+                BR_SUB_T(pr0);
                 act_code = g_post_rhs<GL>(C, V, gl, f, b);
+                BR_SUB_ADD(3, pr0);
                 if (act_code == A_SETUP && o.dq_jac && C->newj) {
                     dq_begin<1, GL>(C, V, gl, f);
                     dqj = 0;
@@ -762,7 +764,9 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
                 if (!lu_fail) delta[0] = g_solve<GL, NM>(a, orig, dinv, n, gl, b[0]);
                 QACC(q_sol_c, c_s);
                 QCLK(c_p);
+                BR_SUB_T(ps_all);
                 act_code = g_post_solve<GL>(C, V, gl, delta, lu_fail);
+                BR_SUB_ADD(13, ps_all);
                 QACC(q_ctl_c, c_p);
             }
             if (act_code == A_DONE) {                                   // ---- results, next reactor

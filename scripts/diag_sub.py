@@ -21,7 +21,8 @@ N = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
 SLOTS = {0: ("LU panel 1", "nsetups"), 1: ("LU panel 2", "nsetups"), 2: ("LU gather", "nsetups"),
          6: ("J multipliers", "nje"), 3: ("ctl post_rhs", "nfe"), 4: ("J entries", "nje"), 5: ("J col write", "nje"),
          7: ("ctl begin_step", "nsteps"), 8: ("ctl conv+err test", "nni"), 9: ("ctl complete+prep", "nsteps"),
-         10: ("ctl ign/unst/tstop", "nsteps"), 11: ("RHS setup", "nfe"), 12: ("RHS production", "nfe")}
+         10: ("ctl ign/unst/tstop", "nsteps"), 11: ("RHS setup", "nfe"), 12: ("RHS production", "nfe"),
+         13: ("ctl post_solve (group engines)", "nni")}
 mech = make_mech(pkg, cfg)
 eng = pkg.Engine(mech)
 lib = ctypes.CDLL(os.environ["BRHIP_LIB"])
