@@ -200,7 +200,7 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
 __device__ __forceinline__ double ud(const LDbl& x) { return (double)x; }
 __device__ __forceinline__ int ui(const __attribute__((address_space(3))) int& x) { return uni((int)x); }
 // Reactor groups: the wavefront engine runs one reactor per wave (group width GW = 64); the group
-// engines (brhip_quad.hpp) two or four per wave, one per 32-lane half or 16-lane DPP row (GW = 32 /
+// engines (brhip_group.hpp) two or four per wave, one per 32-lane half or 16-lane DPP row (GW = 32 /
 // 16), with `lane` the lane within the group. The controller's values are uniform per group: scalar
 // for GW = 64 (readfirstlane: SGPRs, scalar branches), per-lane VGPRs with exec-masked branches for
 // GW < 64; reductions and broadcasts over the group (DPP row butterflies, permlane16 swaps between
@@ -1040,7 +1040,7 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane,
 }
 
 #include "brhip_lane.hpp"   // one reactor per lane (small gas mechanisms)
-#include "brhip_quad.hpp"   // group engines: 4 / 2 reactors per wave (16- / 32-lane groups, n <= 32)
+#include "brhip_group.hpp"   // group engines: 4 / 2 reactors per wave (16- / 32-lane groups, n <= 32)
 
 // ------------------------------------------------------------------------------------
 // the integrator kernel: one reactor per 64-lane wavefront, `rpb` reactors per workgroup
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(256) void k_jac(DevMech M, int N, int rpb, const do
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-// the group-engine instances (brhip_quad.hpp)
+// the group-engine instances (brhip_group.hpp)
 static const void* grp_kernel(int gl, int nm) {
     if (gl == 16) return nm == 9 ? (const void*)k_group<16, 9> : (const void*)k_group<16, 16>;
     return nm == 24 ? (const void*)k_group<32, 24> : (const void*)k_group<32, 32>;
@@ -1434,7 +1434,7 @@ struct br_mech {
     double* lws = nullptr;     // saved Jacobians, slot-major [NM*NM][slots]
     size_t lws_bytes = 0;
     int* queue = nullptr;      // work counter
-    // group engine (brhip_quad.hpp): gl = 0 not eligible, else the group width (16: quad, 32: pair)
+    // group engine (brhip_group.hpp): gl = 0 not eligible, else the group width (16: quad, 32: pair)
     // and the register width NM of k_group<gl, NM>
     int grp_gl = 0, grp_nm = 0, grp_blocks = 0;
     size_t grp_shmem = 0;
@@ -1867,7 +1867,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
             m->lane_blocks = nb * ncu;
         }
     }
-    // ---- group engines (brhip_quad.hpp): 4 reactors per wave for n <= 16, 2 for n <= 32
+    // ---- group engines (brhip_group.hpp): 4 reactors per wave for n <= 16, 2 for n <= 32
     if (n <= 32 && M.nset <= grp::MAX_SETS) {
         m->grp_gl = n <= 16 ? 16 : 32;
         m->grp_nm = n <= 9 ? 9 : (n <= 16 ? 16 : (n <= 24 ? 24 : 32));

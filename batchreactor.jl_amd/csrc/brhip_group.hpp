@@ -1,4 +1,4 @@
-// brhip_quad.hpp -- GROUP ENGINES: two or four reactors per wave for small mechanisms. A reactor
+// brhip_group.hpp -- GROUP ENGINES: two or four reactors per wave for small mechanisms. A reactor
 // occupies a group of GL lanes (GL = 16: one DPP row, n <= 16, "quad", e.g. H2/O2 n = 9, the C2
 // ensemble; GL = 32: one half-wave, 16 < n <= 32, "pair", e.g. the surface-only Ni/CH4 case, n = 20,
 // C4), lane gl of the group holds component gl. Included by brhip.hip after the controller: the same

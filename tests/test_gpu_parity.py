@@ -865,24 +865,26 @@ def test_persistent_grid_matches_static(pkg, gpu, monkeypatch, case, N):
         assert np.array_equal(sd[k], ss[k]), k
 
 
-def test_failure_fraction_matches_cvode(pkg, orc, gpu):
+@pytest.mark.parametrize("dq", [False, True], ids=["analytic", "dq"])
+def test_failure_fraction_matches_cvode(pkg, orc, gpu, dq):
     """C5 gas+surface: a few reactors in 1e3 end with CVODE's CV_ERR_FAILURE (-3, seven consecutive
     error-test failures, in the order-5 phase before ignition). The oracle does the same on the same
     inputs (20000-reactor run: oracle 73, engine 84, 7 in common: which reactors fail is
     rounding-dependent, the rate is the algorithm's). Pinned here: the engine's failure count on the
     first 3000 reactors is within Poisson noise of the oracle's on the same reactors, and every
-    failure is -3 (no other status)."""
+    failure is -3 (no other status) -- with the analytic Jacobian and with CVODE's DQ Jacobian (the
+    reference's setting) on both sides."""
     from batchreactor_amd import ensemble
     pm, om = _mechs(pkg, orc, "gas_surf")
     N = 3000
     T, Asv, U0 = ensemble.make_inputs(pm, "gas_surf", 0, N)
-    U, st = pkg.Engine(pm).integrate(T, Asv, U0, 10.0)
-    _, sto, _ = om.integrate_batch(T, Asv, U0, 10.0, analytic_jac=True, nthreads=16)
+    U, st = pkg.Engine(pm).integrate(T, Asv, U0, 10.0, dq_jacobian=dq)
+    _, sto, _ = om.integrate_batch(T, Asv, U0, 10.0, analytic_jac=not dq, nthreads=16)
     so = np.array([s["status"] for s in sto])
     fg, fo = int(np.sum(st["status"] != 0)), int(np.sum(so != 0))
     assert set(np.unique(st["status"])) <= {0, -3} and set(np.unique(so)) <= {0, -3}
     assert abs(fg - fo) <= 3 * np.sqrt(fo + fg) + 3, (fg, fo)
-    print(f"\n  gas_surf failures on {N}: engine {fg}, oracle {fo}")
+    print(f"\n  gas_surf failures on {N} ({'DQ' if dq else 'analytic'} J): engine {fg}, oracle {fo}")
 
 
 @pytest.mark.parametrize("ndev", [1, 3])
