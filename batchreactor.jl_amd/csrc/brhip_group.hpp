@@ -475,6 +475,11 @@ __device__ __forceinline__ int g_pivot(double a, bool cand, int gl) {
     const unsigned hi = cand ? (unsigned)(bits >> 32) : 0u;
     const unsigned mh = group_umax<GL>(hi);
     const bool top = cand && hi == mh;
+    // usual case: one lane of each (active) group holds the largest high word -- it is the pivot,
+    // and the low-word and lowest-lane rounds are skipped (wave-uniform test; C2 +0.5 %)
+    const unsigned long long tb = __ballot(top);
+    const unsigned gm = (unsigned)(tb >> (threadIdx.x & (64 - GL))) & (GL == 32 ? 0xffffffffu : 0xffffu);
+    if (__ballot(__builtin_popcount(gm) != 1) == 0) return __builtin_ctz(gm);
     const unsigned lo = top ? (unsigned)bits : 0u;
     const unsigned ml = group_umax<GL>(lo);
     const bool top2 = top && lo == ml;
@@ -569,6 +574,12 @@ __device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VT<1, GL>& V, int gl, double (
     return ctl_post_solve<1, GL>(C, V, gl, delta, lu_fail);
 }
 
+#ifndef BR_QJAC_COLS
+// 1 (default): the column-pass Jacobian for gas-only mechanisms too; 0: register rows (g_jac). C2
+// H2/O2: 980.6k vs 902.2k reactors/s, 40.3k vs 78.8k cycles per Jacobian -- g_jac's per-entry scalar
+// compare-and-branch chains, and every cycle of a group's setup idles the other three groups (round 4)
+#define BR_QJAC_COLS 1
+#endif
 #ifndef BR_QWPB
 #define BR_QWPB 4   // waves per workgroup (16 quad / 8 pair reactors); tables staged once per workgroup
 #endif
@@ -739,7 +750,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
             if (act_code == A_SETUP) {
                 if (!jac_ready && C->newj) {                            // analytic Jacobian at y, saved
                     QCLK(c_j);
-                    if (MF(nrs) == 0) {                                 // gas only: register rows
+                    if (MF(nrs) == 0 && !BR_QJAC_COLS) {                // gas only: register rows
                         double jr[NM];
                         g_jac<GL, NM>(tb, sp, kd, fod, gl, jr);
 #pragma unroll
