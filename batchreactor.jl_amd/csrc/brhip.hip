@@ -239,6 +239,12 @@ __device__ __forceinline__ double gbcast(double v, int k) {
     else return lane_pull(v, (int)(threadIdx.x & (64 - GW)) + k);
 }
 
+// analysis builds (BR_ASM_QMARKS): region markers in the 16-lane controller's ISA listing
+#ifdef BR_ASM_QMARKS
+#define BR_QMARK(name) do { if constexpr (GW == 16) asm volatile("; QMARK " #name); } while (0)
+#else
+#define BR_QMARK(name) do { } while (0)
+#endif
 #ifndef BR_CTL_INLINE
 #define BR_CTL_INLINE __forceinline__
 #endif
@@ -579,6 +585,7 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL, GW>& V, int lane,
 template <int CPL, int GW = 64>
 __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL, GW>& V, int lane, const CtlArgs& a) {
     BR_SUB_T(bt0);
+    BR_QMARK(begin_step);
     const double tn = ud(C->tn), hprime = ud(C->hprime), h = ud(C->h);   // read before the V stores
     const int nst = gui<GW>(C->nst), qp = gui<GW>(C->qprime), q = gui<GW>(C->q);
 #pragma unroll
@@ -595,7 +602,9 @@ __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL, GW>& V, int lane, co
         }
         cv_rescale<CPL, GW>(C, V, lane);
     }
+    BR_QMARK(begin_step_attempt);
     begin_attempt<CPL, GW>(C, V, lane, FIRST_CALL);
+    BR_QMARK(begin_step_end);
     BR_SUB_ADD(7, bt0);
 }
 
@@ -747,6 +756,7 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 template <int CPL, int GW = 64>
 __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, double (&delta)[CPL], int lu_fail) {
     BR_SUB_T(ps0);
+    BR_QMARK(ps_start);
     const CtlArgs a = load_args<GW>(C);
     const int n = a.n;
     double ewt[CPL], acor[CPL];
@@ -800,6 +810,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
             nls = 1;
         }
     }
+    BR_QMARK(ps_nflag);
     if (nls != 0) {                                          // cvHandleNFlag
         C->ncfn = gui<GW>(C->ncfn) + 1;
         cv_restore<CPL, GW>(C, V, lane);
@@ -813,6 +824,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
         return A_RHS;
     }
     // ---- cvDoErrorTest
+    BR_QMARK(ps_errtest);
     const double dsm = acnrm * tq2_e;
     const int q = gui<GW>(C->q);
     if (dsm > 1.0) {
@@ -848,6 +860,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
     }
     // ---- cvCompleteStep
     BR_SUB_ADD(8, ps0);
+    BR_QMARK(ps_complete);
     BR_SUB_T(ps1);
     // every controller scalar this part reads, loaded in one batch before the first Nordsieck store
     // (V shares LDS with the controller, so a load placed after a V store cannot be hoisted above
@@ -889,6 +902,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
         C->saved_tq5 = tq5;
     }
     // ---- cvPrepareNextStep
+    BR_QMARK(ps_prepare);
     double eta = 1.0, hprime = h;
     int qprime = q;
     if (etamax == 1.0) {
@@ -941,6 +955,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
     FOR_S z0[s] = V.at(0, s);
     C->eta = eta; C->hprime = hprime; C->qprime = qprime;
     BR_SUB_ADD(9, ps1);
+    BR_QMARK(ps_unstable);
     BR_SUB_T(ps2);
     {   // SciML unstable_check: NaN state (ulimit = inf), or opt-in runaway (br_opts.unstable_factor);
         // first, as in the oracle: an unstable step writes no trace row and no dense output
@@ -956,9 +971,12 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
         FOR_S yl[s] = V.at(V_Y, s);                     // the last RHS was evaluated at y
         trace_row<CPL, GW>(C, a, lane, nst, tn, z0, yl);
     }
+    BR_QMARK(ps_ignition);
     if (a.ign >= 0) track_ignition<CPL, GW>(C, a, lane, tn, z0);
+    BR_QMARK(ps_dense);
     if (a.nout) dense_output<CPL, GW>(C, V, a, lane, tn, h, q, tn);
     // CVode ONE_STEP + tstop handling
+    BR_QMARK(ps_tstop);
     const double troundoff = FUZZ * UROUND * (fabs(tn) + fabs(h));
     if (fabs(tn - tstop) <= troundoff) {                     // CVodeGetDky(tstop, 0)
         if (a.nout) dense_output<CPL, GW>(C, V, a, lane, tn, h, q, tstop);
@@ -984,7 +1002,9 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
     }
     if (nstloc >= a.max_steps) { C->status = BR_ERR_MAXSTEPS; return A_DONE; }
     BR_SUB_ADD(10, ps2);
+    BR_QMARK(ps_to_begin);
     begin_step<CPL, GW>(C, V, lane, a);
+    BR_QMARK(ps_end);
     return A_RHS;
 }
 
