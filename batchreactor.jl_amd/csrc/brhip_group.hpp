@@ -574,6 +574,11 @@ __device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VT<1, GL>& V, int gl, double (
     return ctl_post_solve<1, GL>(C, V, gl, delta, lu_fail);
 }
 
+#ifndef BR_GPRIO
+// issue priority (s_setprio) of a wave while one of its groups runs its Jacobian / LU (the wave's other
+// groups idle meanwhile): C2 993.8k vs 986.7k reactors/s at 2 (mean of two alternations, round 4)
+#define BR_GPRIO 2
+#endif
 #ifndef BR_QJAC_COLS
 // 1 (default): the column-pass Jacobian for gas-only mechanisms too; 0: register rows (g_jac). C2
 // H2/O2: 980.6k vs 902.2k reactors/s, 40.3k vs 78.8k cycles per Jacobian -- g_jac's per-entry scalar
@@ -748,6 +753,9 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
             QACC(q_ctl_c, c_c);
             int lu_fail = 0;
             if (act_code == A_SETUP) {
+#if BR_GPRIO   // a wave with a group in its setup (the others idle) issues first
+                __builtin_amdgcn_s_setprio(BR_GPRIO);
+#endif
                 if (!jac_ready && C->newj) {                            // analytic Jacobian at y, saved
                     QCLK(c_j);
                     if (MF(nrs) == 0 && !BR_QJAC_COLS) {                // gas only: register rows
@@ -768,6 +776,9 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
                 for (int j = 0; j < NM; ++j) jr[j] = jld(j);
                 lu_fail = g_lu<GL, NM>(jr, C->gamma, n, gl, a, orig, dinv);
                 QACC(q_lu_c, c_l);
+#if BR_GPRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
             }
             if (act_code == A_SOLVE || act_code == A_SETUP) {
                 QCLK(c_s);
