@@ -796,6 +796,67 @@ def test_pair_engine_surface(pkg, orc, gpu, monkeypatch):
     assert max(close_states(Up[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(N)) <= 1.0
 
 
+def _h2o2_with_inerts(tmp_path, n):
+    """H2/O2 with inert (reaction-free) species appended from the thermo library up to n components:
+    gas mechanisms of 12, 20 and 30 species for the group engines' other register widths (the bench
+    mechanisms have n = 9 and 53)"""
+    import shutil
+    th = [ln for ln in open(TH).read().split("\n")]
+    names = [ln[:18].split()[0] for ln in th if len(ln) >= 80 and ln[79] == "1"]
+    base = "H2 O2 H2O H O OH HO2 H2O2 N2".split()
+    extra = [s for s in names if s not in base][: n - len(base)]
+    assert len(base) + len(extra) == n
+    src = open(os.path.join(LIB, "h2o2.dat")).read()
+    src = src.replace("ELEMENTS\nH O N\nEND", "ELEMENTS\nH O N C AR\nEND")
+    src = src.replace("H2 O2 H2O H O OH HO2 H2O2 N2", " ".join(base + extra))
+    d = tmp_path / f"lib{n}"
+    d.mkdir()
+    (d / "mech.dat").write_text(src)
+    shutil.copy(TH, d / "therm.dat")
+    return str(d)
+
+
+@pytest.mark.parametrize("n,engine,kernel", [(12, "quad", "k_group<16, 16>"), (20, "pair", "k_group<32, 24>"),
+                                             (30, "pair", "k_group<32, 32>")])
+def test_group_engine_register_widths(pkg, orc, gpu, monkeypatch, tmp_path, n, engine, kernel):
+    """The group engines' other instances (quad with a 16-wide register tile, pair with 24 / 32) on
+    gas-only mechanisms of 12 / 20 / 30 species (H2/O2 plus inert species that only dilute and enter
+    the third-body sums): end states at tight tolerances against the oracle to 1e-6 relative, ignition
+    times within two ignition steps at default tolerances, and the same end states as the wavefront
+    engine."""
+    d = _h2o2_with_inerts(tmp_path, n)
+    pm = pkg.Mechanism.from_files(d, gas_mech="mech.dat")
+    om = orc.Mech(os.path.join(d, "mech.dat"), os.path.join(d, "therm.dat"), None, conv=orc.CONV_REFERENCE)
+    assert pm.n == n
+    monkeypatch.setenv("BRHIP_ENGINE", engine)
+    eng = pkg.Engine(pm)
+    assert eng.engine == engine and eng.kernel_name == kernel, eng.kernel_name
+    N = 48
+    rng = np.random.default_rng(n)
+    T = rng.uniform(1000.0, 1300.0, N)
+    X = np.zeros((N, pm.ng))
+    X[:, pm.gas_species.index("H2")] = 0.3
+    X[:, pm.gas_species.index("O2")] = 0.15
+    X[:, pm.gas_species.index("N2")] = 0.3
+    X[:, len("H2 O2 H2O H O OH HO2 H2O2 N2".split()):] = 0.25 / (n - 9)
+    U0 = np.stack([pm.initial_state(T[i], 1e5, X[i]) for i in range(N)])
+    Asv = np.ones(N)
+    Ug, st = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    assert np.all(st["status"] == 0)
+    for i in range(N):
+        uo, so, _ = om.integrate(T[i], 1.0, U0[i], 1e-2, analytic_jac=True, rtol=1e-10, atol=1e-16)
+        assert so["status"] == 0
+        assert close_states(Ug[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, (n, i)
+    U, st = eng.integrate(T, Asv, U0, 1e-2)
+    for i in range(0, N, 6):
+        uo, so, _ = om.integrate(T[i], 1.0, U0[i], 1e-2, analytic_jac=True)
+        assert abs(st["t_ign"][i] - so["t_ign"]) <= 2 * max(st["ign_dt"][i], so["ign_dt"]) + 1e-4 * so["t_ign"], i
+    monkeypatch.setenv("BRHIP_ENGINE", "wave")
+    Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    assert np.all(sw["status"] == 0)
+    assert max(close_states(Ug[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(N)) <= 1.0
+
+
 def test_lane_engine_deferral(pkg, orc, gpu, monkeypatch):
     """Reactors still running after BRHIP_DEFER_STEPS steps in the lane engine are handed to the
     wavefront engine, which continues them from their last accepted lane state (a CVODE restart at
