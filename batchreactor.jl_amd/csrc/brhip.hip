@@ -1534,9 +1534,23 @@ int br_mech_engine(const br_mech* m) {
 
 int br_mech_launch_info(const br_mech* m, int* rpb, int* waves_per_cu, long long* lds_bytes) {
     if (!m) return fail(BR_ERR_INPUT, "null mechanism");
-    if (rpb) *rpb = m->rpb;
-    if (waves_per_cu) *waves_per_cu = m->waves_per_cu;
-    if (lds_bytes) *lds_bytes = (long long)m->shmem;
+    // the geometry of the engine br_integrate launches (pick_engine), not always the wavefront one
+    const int e = pick_engine(m);
+    const int ncu = m->ncu > 0 ? m->ncu : 1;
+    int r = m->rpb, w = m->waves_per_cu;
+    long long l = (long long)m->shmem;
+    if (e < 0) {          // group engine: BR_QWPB waves per workgroup, 64 / GL reactors per wave
+        r = BR_QWPB * (64 / m->grp_gl);
+        w = m->grp_blocks / ncu * BR_QWPB;
+        l = (long long)m->grp_shmem;
+    } else if (e > 0) {   // reactor-per-lane engine: one wave of 64 reactors per workgroup
+        r = 64;
+        w = m->lane_blocks / ncu;
+        l = (long long)m->lane_shmem;
+    }
+    if (rpb) *rpb = r;
+    if (waves_per_cu) *waves_per_cu = w;
+    if (lds_bytes) *lds_bytes = l;
     return 0;
 }
 

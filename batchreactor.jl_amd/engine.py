@@ -76,8 +76,8 @@ class Engine:
 
     @property
     def launch_info(self) -> dict:
-        """wavefront-engine launch geometry: reactors per workgroup, resident waves per CU, LDS bytes
-        per workgroup (br_mech_launch_info)"""
+        """launch geometry of the engine in use (wave / group / lane): reactors per workgroup, resident
+        waves per CU, LDS bytes per workgroup (br_mech_launch_info)"""
         rpb, wpc, lds = C.c_int(), C.c_int(), C.c_longlong()
         _lib.check(_lib.lib().br_mech_launch_info(self.h, C.byref(rpb), C.byref(wpc), C.byref(lds)))
         return {"reactors_per_workgroup": rpb.value, "waves_per_cu": wpc.value, "lds_bytes_per_workgroup": lds.value}

@@ -182,9 +182,9 @@ int br_mech_info(const br_mech* m, int* ng, int* ns, int* nrg, int* nrs);
  * wavefront engine; env BRHIP_ENGINE = wave | lane | quad | pair forces one where the mechanism is
  * eligible. */
 int br_mech_engine(const br_mech* m);
-/* launch geometry of the wavefront engine for this mechanism (diagnostics): reactors (waves) per
- * workgroup, resident waves per CU (occupancy calculator: VGPRs and LDS), LDS bytes per
- * workgroup (staged tables + one block per reactor). Any pointer may be NULL. */
+/* launch geometry of the engine br_integrate uses for this mechanism (br_mech_engine; diagnostics):
+ * reactors per workgroup, resident waves per CU (occupancy calculator: VGPRs and LDS), LDS bytes
+ * per workgroup (staged tables + one block per reactor or group). Any pointer may be NULL. */
 int br_mech_launch_info(const br_mech* m, int* rpb, int* waves_per_cu, long long* lds_bytes);
 
 /* host-buffer entry points (copy in/out); arrays are reactor-major */

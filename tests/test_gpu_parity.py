@@ -696,6 +696,20 @@ def test_quad_engine_h2o2(pkg, orc, gpu, monkeypatch):
     assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
 
 
+def test_launch_info_follows_the_engine(pkg, orc, gpu, monkeypatch):
+    """br_mech_launch_info (the bench line's roofline.launch) describes the engine br_integrate
+    launches: the quad engine's workgroups hold 4 reactors per wave, the wavefront engine's one."""
+    pm, _ = _mechs(pkg, orc, "h2o2")
+    monkeypatch.setenv("BRHIP_ENGINE", "quad")
+    q = pkg.Engine(pm).launch_info
+    monkeypatch.setenv("BRHIP_ENGINE", "wave")
+    w = pkg.Engine(pm).launch_info
+    assert q["reactors_per_workgroup"] % 4 == 0 and q["reactors_per_workgroup"] >= 4, q
+    assert 1 <= q["waves_per_cu"] <= 32 and 1 <= w["waves_per_cu"] <= 32, (q, w)
+    assert 0 < q["lds_bytes_per_workgroup"] <= 160 * 1024 and 0 < w["lds_bytes_per_workgroup"] <= 160 * 1024
+    assert q != w
+
+
 def test_quad_engine_dq_jacobian(pkg, orc, gpu, monkeypatch):
     """The quad engine with CVODE's DQ Jacobian (br_opts.dq_jacobian, the reference's setting): n RHS per
     Jacobian counted in nfe_dq, states at the 28 output times within the H2/O2-DQ bounds of
