@@ -2390,6 +2390,23 @@ __global__ __launch_bounds__(64) void k_lu_factor_dbg(int N, int n, const double
     pout[(size_t)rid * 64 + lane] = perm;
 }
 }  // namespace
+// device buffers of the diagnostic entry points below, freed on every exit path (HIPCHK returns early)
+namespace {
+struct DevScratch {
+    std::vector<void*> p;
+    ~DevScratch() {
+        for (void* q : p) hipFree(q);
+    }
+    template <class T>
+    hipError_t alloc(T** out, size_t bytes) {
+        void* q = nullptr;
+        const hipError_t e = hipMalloc(&q, bytes);
+        if (e == hipSuccess) { p.push_back(q); *out = (T*)q; }
+        return e;
+    }
+};
+}  // namespace
+
 extern "C" int br_debug_lu_factor(int N, int n, const double* J, const double* gamma, int twice, int stop, double* F,
                                   int* perm) {
     if (N <= 0 || n <= 32 || n > 64) return fail_code_input();
@@ -2397,11 +2414,12 @@ extern "C" int br_debug_lu_factor(int N, int n, const double* J, const double* g
     const size_t lw = lu_ws_doubles(nmax);
     double *dJ, *dg, *dws, *dF;
     int* dp;
-    HIPCHK(hipMalloc(&dJ, (size_t)N * n * n * 8));
-    HIPCHK(hipMalloc(&dg, (size_t)N * 8));
-    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * WAVE + lw) * 8));
-    HIPCHK(hipMalloc(&dF, (size_t)N * lw * 8));
-    HIPCHK(hipMalloc(&dp, (size_t)N * 64 * 4));
+    DevScratch S;
+    HIPCHK(S.alloc(&dJ, (size_t)N * n * n * 8));
+    HIPCHK(S.alloc(&dg, (size_t)N * 8));
+    HIPCHK(S.alloc(&dws, (size_t)N * (nmax * WAVE + lw) * 8));
+    HIPCHK(S.alloc(&dF, (size_t)N * lw * 8));
+    HIPCHK(S.alloc(&dp, (size_t)N * 64 * 4));
     HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, twice, dws, dF, dp); };
@@ -2413,7 +2431,6 @@ extern "C" int br_debug_lu_factor(int N, int n, const double* J, const double* g
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(F, dF, (size_t)N * lw * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(perm, dp, (size_t)N * 64 * 4, hipMemcpyDeviceToHost));
-    hipFree(dJ); hipFree(dg); hipFree(dws); hipFree(dF); hipFree(dp);
     return 0;
 }
 
@@ -2423,12 +2440,13 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     const int nmax = n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : (n <= 64 ? 64 : 72)));
     double *dJ, *dg, *db, *dx, *dws;
     int* df;
-    HIPCHK(hipMalloc(&dJ, (size_t)N * n * n * 8));
-    HIPCHK(hipMalloc(&dg, (size_t)N * 8));
-    HIPCHK(hipMalloc(&db, (size_t)N * n * 8));
-    HIPCHK(hipMalloc(&dx, (size_t)N * n * 8));
-    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
-    HIPCHK(hipMalloc(&df, (size_t)N * 4));
+    DevScratch S;
+    HIPCHK(S.alloc(&dJ, (size_t)N * n * n * 8));
+    HIPCHK(S.alloc(&dg, (size_t)N * 8));
+    HIPCHK(S.alloc(&db, (size_t)N * n * 8));
+    HIPCHK(S.alloc(&dx, (size_t)N * n * 8));
+    HIPCHK(S.alloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
+    HIPCHK(S.alloc(&df, (size_t)N * 4));
     HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(db, b, (size_t)N * n * 8, hipMemcpyHostToDevice));
@@ -2440,7 +2458,6 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(x, dx, (size_t)N * n * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));
-    hipFree(dJ); hipFree(dg); hipFree(db); hipFree(dx); hipFree(dws); hipFree(df);
     return 0;
 }
 
@@ -2451,12 +2468,13 @@ extern "C" int br_debug_lu_solve_mf(int N, int n, const double* J, const double*
     const int nmax = n <= 56 ? 56 : 64;
     double *dJ, *dg, *db, *dx, *dws;
     int* df;
-    HIPCHK(hipMalloc(&dJ, (size_t)N * n * n * 8));
-    HIPCHK(hipMalloc(&dg, (size_t)N * 8));
-    HIPCHK(hipMalloc(&db, (size_t)N * n * 8));
-    HIPCHK(hipMalloc(&dx, (size_t)N * n * 8));
-    HIPCHK(hipMalloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
-    HIPCHK(hipMalloc(&df, (size_t)N * 4));
+    DevScratch S;
+    HIPCHK(S.alloc(&dJ, (size_t)N * n * n * 8));
+    HIPCHK(S.alloc(&dg, (size_t)N * 8));
+    HIPCHK(S.alloc(&db, (size_t)N * n * 8));
+    HIPCHK(S.alloc(&dx, (size_t)N * n * 8));
+    HIPCHK(S.alloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
+    HIPCHK(S.alloc(&df, (size_t)N * 4));
     HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(db, b, (size_t)N * n * 8, hipMemcpyHostToDevice));
@@ -2465,7 +2483,6 @@ extern "C" int br_debug_lu_solve_mf(int N, int n, const double* J, const double*
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(x, dx, (size_t)N * n * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));
-    hipFree(dJ); hipFree(dg); hipFree(db); hipFree(dx); hipFree(dws); hipFree(df);
     return 0;
 }
 

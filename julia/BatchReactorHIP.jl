@@ -55,9 +55,12 @@ struct BrOpts
     yout::Ptr{Float64}          # [N][nout][n]
     dq_jacobian::Cint           # 1: CVODE's DQ Jacobian (cvLsDenseDQJac, the reference's setting), every engine
 end
-BrOpts(; rtol=1e-6, atol=1e-10, max_steps=100_000, device=0, ignition_species=0) =
-    BrOpts(rtol, atol, Cint(max_steps), Cint(device), 0.0, Cint(0), 0.0, Cint(ignition_species), Cint(0),
-           C_NULL, C_NULL, Cint(0))
+# dq_jacobian=true selects CVODE's difference-quotient Jacobian, the reference's CVODE_BDF() setting
+# (src/BatchReactor.jl:140,:204); the default is the analytic Jacobian
+BrOpts(; rtol=1e-6, atol=1e-10, max_steps=100_000, device=0, hmax=0.0, unstable_factor=0.0, ignition_species=0,
+       dq_jacobian::Bool=false) =
+    BrOpts(rtol, atol, Cint(max_steps), Cint(device), Float64(hmax), Cint(0), Float64(unstable_factor),
+           Cint(ignition_species), Cint(0), C_NULL, C_NULL, Cint(dq_jacobian))
 
 # br_stats rows of the [NSTAT x N] matrix returned below
 const STAT_FIELDS = (:nsteps, :nfe, :nje, :nsetups, :nni, :ncfn, :netf, :status, :cyc_total, :cyc_rhs, :cyc_jac,
@@ -135,15 +138,33 @@ end
 `gas_mech == ""`: surface-only run, gas species from `gasphase` (space-separated, the <gasphase> tag)."""
 function compile_mechanism(gas_mech::AbstractString, therm::AbstractString, surf_mech::AbstractString="";
                            gasphase::AbstractString="", conv::Integer=CONV_REFERENCE, device::Integer=0)
+    h, d, names, molwt, theta0 = _parse_host(gas_mech, therm, surf_mech; gasphase=gasphase, conv=conv)
+    m = C_NULL
+    try
+        m = mech_create(d, device)
+        dd = d[]
+        dm = DeviceMech(h, m, Int(device), Int(dd.ng), Int(dd.ns), Int(dd.nrg), Int(dd.nrs), names, molwt, theta0)
+        finalizer(_free!, dm)
+        return dm
+    catch
+        m != C_NULL && ccall((:br_mech_destroy, lib), Cint, (Ptr{Cvoid},), m)
+        ccall((:br_host_mech_free, lib), Cint, (Ptr{Cvoid},), h)
+        rethrow()
+    end
+end
+
+"""The host half of compile_mechanism (br_mech_parse; no GPU): the br_host_mech handle (the caller
+frees it with br_host_mech_free), its br_mech_desc, species names, molecular weights and theta0."""
+function _parse_host(gas_mech::AbstractString, therm::AbstractString, surf_mech::AbstractString="";
+                     gasphase::AbstractString="", conv::Integer=CONV_REFERENCE)
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:br_mech_parse, lib), Cint, (Cstring, Cstring, Cstring, Cstring, Cint, Ref{Ptr{Cvoid}}),
                 gas_mech, therm, surf_mech, gasphase, conv, h))
-    # every step after br_mech_parse may throw (check): free what exists so far, then rethrow
-    m = C_NULL
+    # every step after br_mech_parse may throw (check): free the handle, then rethrow
     try
         d = Ref{BrMechDesc}()
         check(ccall((:br_host_mech_desc, lib), Cint, (Ptr{Cvoid}, Ref{BrMechDesc}), h[], d))
-        ng, ns, nrg, nrs = Int(d[].ng), Int(d[].ns), Int(d[].nrg), Int(d[].nrs)
+        ng, ns = Int(d[].ng), Int(d[].ns)
         buf = zeros(UInt8, 64)
         names = String[]
         for i in 0:(ng + ns - 1)
@@ -153,12 +174,8 @@ function compile_mechanism(gas_mech::AbstractString, therm::AbstractString, surf
         molwt = copy(unsafe_wrap(Array, d[].molwt, ng))
         theta0 = zeros(ns)
         check(ccall((:br_host_mech_theta0, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], theta0))
-        m = mech_create(d, device)
-        dm = DeviceMech(h[], m, Int(device), ng, ns, nrg, nrs, names, molwt, theta0)
-        finalizer(_free!, dm)
-        return dm
+        return h[], d, names, molwt, theta0
     catch
-        m != C_NULL && ccall((:br_mech_destroy, lib), Cint, (Ptr{Cvoid},), m)
         ccall((:br_host_mech_free, lib), Cint, (Ptr{Cvoid},), h[])
         rethrow()
     end
@@ -259,10 +276,12 @@ end
 on the HIP engine: reads batch.xml, compiles the mechanism library files natively, integrates the
 reactor (CVODE_BDF restatement, rtol 1e-6, atol 1e-10), writes gas_profile.{dat,csv} and
 surface_covg.{dat,csv} next to the input and returns Symbol(retcode). sens=true returns
-(params, prob, t_span) with prob.f = residual! evaluated on the GPU (br_rhs)."""
+(params, prob, t_span) with prob.f = residual! evaluated on the GPU (br_rhs). dq_jacobian=true
+runs CVODE's difference-quotient Jacobian, the reference's own CVODE_BDF() setting (:204-210);
+the default is the analytic Jacobian (same step-control algorithm)."""
 function batch_reactor(input_file::AbstractString, lib_dir::AbstractString; sens::Bool=false,
                        surfchem::Bool=false, gaschem::Bool=false, device::Integer=0,
-                       conv::Integer=CONV_REFERENCE, max_steps::Integer=100_000)
+                       conv::Integer=CONV_REFERENCE, max_steps::Integer=100_000, dq_jacobian::Bool=false)
     inp = read_batch_xml(input_file)
     gm = gaschem ? joinpath(lib_dir, inp.gas_mech) : ""
     sm = surfchem ? joinpath(lib_dir, inp.surface_mech) : ""
@@ -276,7 +295,7 @@ function batch_reactor(input_file::AbstractString, lib_dir::AbstractString; sens
         t_span = (0.0, inp.time)
         return params, (f=residual!, u0=u0, tspan=t_span, p=params), t_span
     end
-    opts = BrOpts(max_steps=max_steps, ignition_species=ignition_species(dm))
+    opts = BrOpts(max_steps=max_steps, ignition_species=ignition_species(dm), dq_jacobian=dq_jacobian)
     cap = min(4096, max_steps)
     stats, trace = integrate_traced!(dm.m, [inp.T], [inp.Asv], reshape(copy(u0), n, 1), [inp.time]; cap=cap, opts=opts)
     nst = Int(stats[1, 1])
@@ -299,10 +318,23 @@ function rhs(dm::DeviceMech, T::Real, Asv::Real, u::AbstractVector)
 end
 
 """batch_reactor(inlet_comp, T, p, time; Asv, chem, thermo_obj, md) (src/BatchReactor.jl:86-147):
-returns (t = [0, time], Dict(species => x_end)); the mechanism is a DeviceMech from compile_mechanism."""
-function batch_reactor(inlet_comp::AbstractDict, T::Real, p::Real, time::Real; Asv::Real=1.0, md::DeviceMech)
+returns (t = [0, time], Dict(species => x_end)); the mechanism is a DeviceMech from compile_mechanism.
+`chem` is the reference's Chemistry(surfchem, gaschem, userchem, udf) (ReactionCommons) or this
+module's `Chemistry`: any object with `surfchem` / `gaschem` fields; the flags must describe `md`
+(gas reactions present iff gaschem, surface species present iff surfchem; the reference takes one
+chemistry per call, :102-127). `thermo_obj` (IdealGas.SpeciesThermoObj in the reference, :131) is
+accepted for call compatibility: `md` carries the NASA-7 tables and molecular weights of the same
+species, matched by name. dq_jacobian as in the file-driven method."""
+function batch_reactor(inlet_comp::AbstractDict, T::Real, p::Real, time::Real; Asv::Real=1.0, chem=nothing,
+                       thermo_obj=nothing, md::DeviceMech, dq_jacobian::Bool=false)
+    if chem !== nothing
+        sc, gc = Bool(getproperty(chem, :surfchem)), Bool(getproperty(chem, :gaschem))
+        (sc || gc) || error("chem: neither surfchem nor gaschem is set")
+        gc == (md.nrg > 0) || error("chem.gaschem = $gc but the mechanism has $(md.nrg) gas reactions")
+        sc == (md.ns > 0) || error("chem.surfchem = $sc but the mechanism has $(md.ns) surface species")
+    end
     u = reshape(initial_state(md, T, p, inlet_comp), ncomp(md), 1)
-    stats = integrate!(md.m, [Float64(T)], [Float64(Asv)], u, [Float64(time)])
+    stats = integrate!(md.m, [Float64(T)], [Float64(Asv)], u, [Float64(time)]; opts=BrOpts(dq_jacobian=dq_jacobian))
     stats[8, 1] == 0 || error("integration failed with status $(stats[8, 1])")
     xf = state_to_molefrac(md, u[:, 1])
     return [0.0, Float64(time)], Dict(zip(gas_species(md), xf))
@@ -335,6 +367,135 @@ function integrate_multi!(mechs::Vector{Ptr{Cvoid}}, T, Asv, u::Matrix{Float64},
     return stats
 end
 
-export batch_reactor, batch_reactor_ensemble, compile_mechanism, read_batch_xml, DeviceMech
+# ---------------------------------------------------------------------------------------------
+# user-defined chemistry (src/BatchReactor.jl:42-54, :197-200, :358-360, :371-372)
+# ---------------------------------------------------------------------------------------------
+"""ReactionCommons.Chemistry(surfchem, gaschem, userchem, udf) (src/BatchReactor.jl:52,:68)."""
+struct Chemistry
+    surfchem::Bool
+    gaschem::Bool
+    userchem::Bool
+    udf::Function
+end
+
+"""ReactionCommons.UserDefinedState(T, p, mole_frac, molwt, species, source) as the reference builds
+it (:197-200): the udf fills `source` [mol/m3/s]; du = source .* molwt (:371-372)."""
+mutable struct UserDefinedState
+    T::Float64
+    p::Float64
+    mole_frac::Vector{Float64}
+    molwt::Vector{Float64}
+    species::Vector{String}
+    source::Vector{Float64}
+end
+
+"""One adaptive step sequence of the Dormand-Prince 5(4) pair (FSAL, WRMS error norm with the
+reference's tolerances) for du/dt = f(t) on the host. In the reference's userchem path residual!
+never updates the state the udf sees (u_state keeps the inlet T, p and mole fractions, :358-360), so
+the source cannot depend on u: the ODE is a quadrature, not stiff. Calls `rowcb(t, u)` after every
+accepted step (save_data's callback, :208-210) and returns (t_end, u, success)."""
+function _dopri_host(f!, u0::Vector{Float64}, tf::Float64; rtol=1e-6, atol=1e-10, max_steps=100_000,
+                     rowcb=(t, u) -> nothing)
+    c = (0.0, 1/5, 3/10, 4/5, 8/9, 1.0, 1.0)
+    a = ((), (1/5,), (3/40, 9/40), (44/45, -56/15, 32/9), (19372/6561, -25360/2187, 64448/6561, -212/729),
+         (9017/3168, -355/33, 46732/5247, 49/176, -5103/18656), (35/384, 0.0, 500/1113, 125/192, -2187/6784, 11/84))
+    e = (71/57600, 0.0, -71/16695, 71/1920, -17253/339200, 22/525, -1/40)   # b5 - b4
+    n = length(u0)
+    u = copy(u0)
+    k = [zeros(n) for _ in 1:7]
+    t = 0.0
+    f!(k[1], u, t)
+    h = tf > 0 ? min(tf, 1e-6 * max(tf, 1.0)) : 0.0
+    rowcb(t, u)
+    nst = 0
+    while t < tf
+        nst >= max_steps && return t, u, false
+        h = min(h, tf - t)
+        for s in 2:7
+            y = copy(u)
+            for j in 1:(s - 1)
+                y .+= h * a[s][j] .* k[j]
+            end
+            f!(k[s], y, t + c[s] * h)
+        end
+        unew = copy(u)
+        for j in 1:6
+            unew .+= h * a[7][j] .* k[j]
+        end
+        err = zeros(n)
+        for j in 1:7
+            err .+= h * e[j] .* k[j]
+        end
+        w = atol .+ rtol .* max.(abs.(u), abs.(unew))
+        en = sqrt(sum((err ./ w) .^ 2) / max(n, 1))
+        if en <= 1.0 || h <= 16 * eps(max(abs(t), 1.0))
+            t = (tf - t - h <= 16 * eps(max(abs(tf), 1.0))) ? tf : t + h
+            u = unew
+            k[1] .= k[7]                                                   # FSAL
+            nst += 1
+            rowcb(t, u)
+        end
+        h *= en == 0 ? 5.0 : clamp(0.9 * en^(-1 / 5), 0.2, 5.0)
+    end
+    return t, u, true
+end
+
+"""batch_reactor(input_file, lib_dir, user_defined::Function; sens=false) (src/BatchReactor.jl:51-54):
+user-defined chemistry. The gas species are batch.xml's <gasphase> (no mechanism files, :256-260;
+molecular weights from lib_dir/therm.dat through br_mech_parse, no GPU). The udf is called with a
+UserDefinedState whose T, p and mole fractions stay at the inlet values, as in the reference; its
+`source` drives du = source .* molwt. Host code by nature (a Julia callback cannot run in a HIP
+kernel): integrated on the host (_dopri_host), one output row per accepted step in the save_data
+format (t, T, p, rho = sum(u), the state's mole fractions; :383-402). sens=true returns
+(params, prob, t_span) with prob.f = residual! (:205-207)."""
+function batch_reactor(input_file::AbstractString, lib_dir::AbstractString, user_defined::Function;
+                       sens::Bool=false, max_steps::Integer=100_000)
+    inp = read_batch_xml(input_file)
+    h, _, names, molwt, _ = _parse_host("", joinpath(lib_dir, "therm.dat"), ""; gasphase=inp.gasphase)
+    ccall((:br_host_mech_free, lib), Cint, (Ptr{Cvoid},), h)
+    ng = length(names)
+    v = zeros(ng)
+    for (k, val) in inp.comp
+        i = findfirst(==(uppercase(String(k))), names)
+        i === nothing || (v[i] = val)
+    end
+    x = inp.comp_is_mass ? (t = v ./ molwt; t ./ sum(t)) : v
+    Mb = sum(x .* molwt)
+    rho = inp.p * Mb / (R_GAS * inp.T)
+    u0 = (x .* molwt ./ Mb) .* rho                                          # get_solution_vector (:224-232)
+    state = UserDefinedState(inp.T, inp.p, copy(x), molwt, names, zeros(ng))
+    chem = Chemistry(false, false, true, user_defined)
+    residual! = (du, u, p, t) -> (user_defined(state); du[1:ng] .= state.source[1:ng] .* molwt; nothing)
+    if sens
+        params = (s_state=nothing, g_state=nothing, u_state=state, thermo=(molwt=molwt, species=names),
+                  smd=nothing, gmd=nothing, cp=(Asv=inp.Asv, T=inp.T), chem=chem)
+        t_span = (0.0, inp.time)
+        return params, (f=residual!, u0=u0, tspan=t_span, p=params), t_span
+    end
+    folder = dirname(abspath(input_file))
+    g_dat = open(joinpath(folder, "gas_profile.dat"), "w")
+    s_dat = open(joinpath(folder, "surface_covg.dat"), "w")
+    g_csv = open(joinpath(folder, "gas_profile.csv"), "w")
+    s_csv = open(joinpath(folder, "surface_covg.csv"), "w")
+    ok = false
+    try
+        hdr = vcat(["t", "T", "p", "rho"], names)
+        write(g_dat, join([@sprintf("%10s\t", hh) for hh in hdr]), "\n")
+        write(g_csv, join(hdr, ","), "\n")
+        row = (t, u) -> begin
+            vals = vcat([t, state.T, state.p, sum(u)], state.mole_frac)
+            write(g_dat, join([@sprintf("%.4e\t", vv) for vv in vals]), "\n")
+            write(g_csv, join(string.(vals), ","), "\n")
+        end
+        f! = (du, u, t) -> residual!(du, u, nothing, t)
+        _, _, ok = _dopri_host(f!, u0, Float64(inp.time); max_steps=max_steps, rowcb=row)
+    finally
+        close(g_dat); close(s_dat); close(g_csv); close(s_csv)
+    end
+    return ok ? Symbol("Success") : Symbol("MaxIters")
+end
+
+export batch_reactor, batch_reactor_ensemble, compile_mechanism, read_batch_xml, DeviceMech, Chemistry,
+       UserDefinedState, BrOpts
 
 end # module

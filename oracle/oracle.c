@@ -605,7 +605,9 @@ static void falloff(const orc_mech* m, const grxn_t* r, const tcache_t* c, int i
  * hash of (call, reaction) -- the few-ulp differences of an RHS implementation that evaluates the
  * same formulas in another order, amplified by CVODE's DQ Jacobian (inc ~ 1e-8 |y|). 0 = off. */
 static double g_rop_jitter = 0.0;
-static unsigned long long g_rop_calls = 0;
+/* per thread, and touched only while the jitter is on: a shared counter written by every OpenMP thread on
+ * every RHS call was a data race and put all threads on one cache line (16-thread baseline -80 %, r04) */
+static _Thread_local unsigned long long g_rop_calls = 0;
 void orc_set_rop_jitter(double eps) { g_rop_jitter = eps; }
 static inline double rop_jit(int i) {
     unsigned long long h = (g_rop_calls * 0x9E3779B97F4A7C15ull) ^ ((unsigned long long)i * 0xC2B2AE3D27D4EB4Full);
@@ -633,7 +635,7 @@ static void gas_rop(const orc_mech* m, const tcache_t* tc, const double* c, doub
         }
         q[i] = g_rop_jitter != 0.0 ? D * (1.0 + rop_jit(i)) : D;
     }
-    g_rop_calls++;
+    if (g_rop_jitter != 0.0) g_rop_calls++;
 }
 
 static void surf_rop(const orc_mech* m, const tcache_t* tc, const double* c, const double* th, double* q) {
@@ -655,7 +657,7 @@ static void surf_rop(const orc_mech* m, const tcache_t* tc, const double* c, con
         }
         q[i] = g_rop_jitter != 0.0 ? k * P * (1.0 + rop_jit(100000 + i)) : k * P;
     }
-    g_rop_calls++;
+    if (g_rop_jitter != 0.0) g_rop_calls++;
 }
 
 static void conc_from_x(const orc_mech* m, double T, double p, const double* x, double* c) {

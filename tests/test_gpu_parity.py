@@ -1001,3 +1001,103 @@ def test_native_cli_matches_python_host(pkg, gpu, tmp_path, scenario, flags, che
     assert pkg.batch_reactor(str(b / "batch.xml"), LIB, **chem) == "Success"
     for f in ("gas_profile.dat", "gas_profile.csv", "surface_covg.dat", "surface_covg.csv"):
         assert (a / f).read_text() == (b / f).read_text(), f
+
+
+_SMALL_SURF = """<?xml version="1.0" encoding="ISO-8859-1"?>
+<surface_chemisrty unit="kJ/mol" name="h2coni">
+	<species>(ni) H(ni) O(ni) H2O(ni) OH(ni) CO(ni) </species>
+	<site name="(ni)">
+		<coordination>co(ni)=1.0</coordination>
+		<density unit="mol/cm2">2.66e-09</density>
+		<initial>h2o(ni)=0.4,(ni)=0.6 </initial>
+	</site>
+	<stick>
+		<rxn id="1" >h2 + (ni) + (ni) => h(ni) + h(ni) 	@ 1.0000e-2 </rxn>
+		<rxn id="2" >o2 + (ni) + (ni) => o(ni) + o(ni) 	@ 1.0000e-2 </rxn>
+		<rxn id="4" >h2o + (ni) => h2o(ni)              	@ 1.0000e-1 </rxn>
+		<rxn id="6" >co + (ni) => co(ni)                	@ 5.0000e-1 </rxn>
+	</stick>
+	<arrhenius>
+		<rxn id="7"  >h(ni) + h(ni) => (ni) + (ni) + h2 	@ 2.545e+19	0.0	81.21	</rxn>
+		<rxn id="8"  >o(ni) + o(ni) => (ni) + (ni) + o2 	@ 4.283e+23	0.0	474.95	</rxn>
+		<rxn id="10" >h2o(ni)  => (ni) + h2o		@ 3.732e+12	0.0 	60.79	</rxn>
+		<rxn id="12" >co(ni)  => (ni) + co 		@ 3.563e+11	0.0	111.27	</rxn>
+		<rxn id="13" >o(ni) + h(ni) => oh(ni) + (ni)	@ 5.000e+22	0.0	97.90	</rxn>
+		<rxn id="14" >oh(ni) + (ni) => o(ni) + h(ni)	@ 1.781e+21	0.0	36.09	</rxn>
+		<rxn id="15" >oh(ni) + h(ni) => h2o(ni) + (ni)	@ 3.000e+20	0.0	42.70	</rxn>
+		<rxn id="16" >h2o(ni) + (ni) => oh(ni) + h(ni)	@ 2.271e+21	0.0	91.76	</rxn>
+		<rxn id="17" >oh(ni) + oh(ni) => o(ni) + h2o(ni)	@ 3.000e+21	0.0	100.00	</rxn>
+		<rxn id="18" >o(ni) + h2o(ni) => oh(ni) + oh(ni)	@ 6.373e+23	0.0	210.86	</rxn>
+	</arrhenius>
+	<coverage id="12">co(ni)=-50</coverage>
+</surface_chemisrty>
+"""
+SMALL_SURF_GAS = ["H2", "O2", "H2O", "CO", "N2"]
+
+
+def _small_surface_mech(pkg, orc, tmp_path):
+    """A surface mechanism small enough for the quad engine (n = 5 gas + 6 surface = 11 <= 16): the
+    H2/O2/H2O/CO subset of the reference's ch4ni.xml (tests/golden/lib; same rate constants,
+    sticking reactions, the coverage-dependent CO desorption), written to a scratch library."""
+    import shutil
+    d = tmp_path / "smallsurf"
+    d.mkdir()
+    (d / "h2coni.xml").write_text(_SMALL_SURF)
+    shutil.copy(TH, d / "therm.dat")
+    pm = pkg.Mechanism.from_files(str(d), surface_mech="h2coni.xml", gasphase=SMALL_SURF_GAS)
+    om = orc.Mech(None, str(d / "therm.dat"), str(d / "h2coni.xml"), gas_species=SMALL_SURF_GAS,
+                  conv=orc.CONV_REFERENCE)
+    return pm, om
+
+
+def test_quad_engine_surface_chemistry(pkg, orc, gpu, monkeypatch, tmp_path):
+    """The quad engine (k_group<16, NM>, the default for mechanisms with n <= 16) on SURFACE chemistry:
+    sticking coefficients, coverage-dependent activation, the Asv assembly of src/BatchReactor.jl:345,
+    on a reduced Ni mechanism with n = 11. Default engine selection picks it; against the oracle at
+    tight tolerances (end states to 1e-6 relative, analytic and DQ Jacobians), at default tolerances
+    (2x the oracle's own u0-perturbation spread at the 28 output times, tests/parity_bands.py; step
+    counts to 35 % / 3 %), and the
+    same end states as the wavefront engine."""
+    pm, om = _small_surface_mech(pkg, orc, tmp_path)
+    assert pm.n == 11 and pm.ns == 6
+    monkeypatch.delenv("BRHIP_ENGINE", raising=False)
+    eng = pkg.Engine(pm)
+    assert eng.engine == "quad" and eng.kernel_name.startswith("k_group<16,"), (eng.engine, eng.kernel_name)
+    N = 96
+    rng = np.random.default_rng(17)
+    T = rng.uniform(800.0, 1100.0, N)
+    X = np.zeros((N, pm.ng))
+    X[:, 0] = rng.uniform(0.05, 0.3, N)          # H2
+    X[:, 1] = rng.uniform(0.05, 0.2, N)          # O2
+    X[:, 2] = rng.uniform(0.0, 0.1, N)           # H2O
+    X[:, 3] = rng.uniform(0.0, 0.05, N)          # CO
+    X[:, 4] = 1.0 - X[:, :4].sum(1)              # N2
+    U0 = np.stack([pm.initial_state(T[i], 1e5, X[i]) for i in range(N)])     # theta0 from <initial>
+    Asv = np.exp(rng.uniform(0, np.log(100), N))
+    for dq in (False, True):
+        U, st = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16, dq_jacobian=dq)
+        assert np.all(st["status"] == 0), (dq, np.unique(st["status"]))
+        if dq:
+            assert np.all(st["nfe_dq"] == st["nje"] * pm.n)
+        for i in range(N):
+            uo, so, _ = om.integrate(T[i], Asv[i], U0[i], 1e-2, analytic_jac=not dq, rtol=1e-10, atol=1e-16)
+            assert so["status"] == 0
+            assert close_states(U[i], uo, rtol=1e-6, floor=1e-14) <= 1.0, (dq, i)
+    U, st = eng.integrate(T, Asv, U0, 10.0, tout=OUT_T)
+    assert np.all(st["status"] == 0)
+    bounds = BOUNDS[("small_surf", False)]
+    nst_o = 0
+    for i in range(N):
+        uo, so, Yo = om.integrate_out(T[i], Asv[i], U0[i], 10.0, OUT_T, analytic_jac=True)
+        assert so["status"] == 0
+        eb = _band_errors(st["yout"][i], Yo, float("nan"))
+        assert eb[0] <= bounds[0], (i, eb)
+        assert abs(st["nsteps"][i] - so["nsteps"]) <= 0.35 * so["nsteps"], (i, st["nsteps"][i], so["nsteps"])
+        nst_o += so["nsteps"]
+    assert abs(st["nsteps"].sum() / nst_o - 1) <= 0.03, (st["nsteps"].sum(), nst_o)
+    Uq, _ = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    monkeypatch.setenv("BRHIP_ENGINE", "wave")
+    assert eng.engine == "wave"
+    Uw, sw = eng.integrate(T, Asv, U0, 1e-2, rtol=1e-10, atol=1e-16)
+    assert np.all(sw["status"] == 0)
+    assert max(close_states(Uq[i], Uw[i], rtol=1e-6, floor=1e-14) for i in range(N)) <= 1.0

@@ -1,0 +1,245 @@
+"""Mechanical checks of the Julia drop-in (julia/BatchReactorHIP.jl) against the C-ABI it binds.
+
+Julia is not installed in this image, so the module cannot run here. What can go wrong silently in a
+`ccall` binding is layout and signature drift, and that is checked on the text: every
+`ccall((:br_*, lib), Ret, (ArgTypes...), ...)` against the prototype in include/brhip.h (arity, each
+argument's C type against the Julia type allowed to carry it), every Julia struct that mirrors a C
+struct field for field (names, order, types), the br_stats row order, the constants, and the ctypes
+mirror in batchreactor.jl_amd/_lib.py against the same header. Plus the reference's public methods
+(src/BatchReactor.jl:51-54, :67-70, :86) and the keywords they take.
+"""
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HDR = os.path.join(ROOT, "include", "brhip.h")
+JL = os.path.join(ROOT, "julia", "BatchReactorHIP.jl")
+
+
+def _strip_c_comments(s):
+    s = re.sub(r"/\*.*?\*/", " ", s, flags=re.S)
+    return re.sub(r"//[^\n]*", " ", s)
+
+
+def _header():
+    src = _strip_c_comments(open(HDR).read())
+    defines = {m.group(1): m.group(2).strip() for m in re.finditer(r"#define\s+(\w+)\s+([^\n]+)", src)}
+    structs = {}
+    for m in re.finditer(r"typedef\s+struct\s+(\w+)\s*\{(.*?)\}\s*(\w+)\s*;", src, re.S):
+        fields = []
+        for decl in m.group(2).split(";"):
+            decl = " ".join(decl.split())
+            if not decl:
+                continue
+            dm = re.match(r"^(.*?)(\w+(?:\s*\[[^\]]+\])*(?:\s*,\s*\w+(?:\s*\[[^\]]+\])*)*)$", decl)
+            base, names = dm.group(1).strip(), dm.group(2)
+            for nm in names.split(","):
+                nm = nm.strip()
+                ptr = ""
+                while nm.startswith("*"):
+                    ptr += "*"
+                    nm = nm[1:].strip()
+                dims = re.findall(r"\[([^\]]+)\]", nm)
+                fields.append((nm.split("[")[0].strip(), (base + ptr).replace(" ", ""), dims))
+        structs[m.group(3)] = fields
+    protos = {}
+    body = re.sub(r"typedef[^;]*\{.*?\}[^;]*;", " ", src, flags=re.S)
+    body = re.sub(r"(?m)^\s*#.*$", " ", body)
+    body = re.sub(r'extern\s+"C"\s*\{|^\s*\}\s*$', " ", body, flags=re.M)
+    for stmt in body.split(";"):
+        m = re.match(r"^\s*([\w\s\*]+?)\b(br_\w+)\s*\(([^)]*)\)\s*$", stmt, re.S)
+        if not m:
+            continue
+        ret = " ".join(m.group(1).split())
+        args = []
+        a = m.group(3).strip()
+        if a and a != "void":
+            for p in a.split(","):
+                p = " ".join(p.split())
+                t = re.sub(r"\b\w+$", "", p).strip() if re.search(r"[\w\*]\s+\w+$", p) else p
+                args.append(t.replace(" *", "*").replace("* ", "*"))
+        protos[m.group(2)] = (ret.replace(" ", ""), [a.replace(" ", "") for a in args])
+    return defines, structs, protos
+
+
+def _balanced(s, i):
+    """index just past the parenthesis group starting at s[i] == '('"""
+    depth = 0
+    for j in range(i, len(s)):
+        if s[j] in "({":
+            depth += 1
+        elif s[j] in ")}":
+            depth -= 1
+            if depth == 0:
+                return j + 1
+    raise ValueError("unbalanced")
+
+
+def _split_top(s):
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "({[":
+            depth += 1
+        elif ch in ")}]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _julia():
+    raw = open(JL).read()
+    src = re.sub(r"#[^\n]*", "", re.sub(r'"""(.*?)"""', '""', raw, flags=re.S))
+    calls = []
+    for m in re.finditer(r"ccall\(", src):
+        end = _balanced(src, m.end() - 1)
+        parts = _split_top(src[m.end():end - 1])
+        sym = re.match(r"\(:(\w+),\s*lib\)", parts[0]).group(1)
+        ret = parts[1]
+        tup = parts[2].strip()
+        assert tup.startswith("(") and tup.endswith(")"), tup
+        types = [t for t in _split_top(tup[1:-1]) if t]
+        calls.append((sym, ret, types, len(parts) - 3))
+    structs = {}
+    for m in re.finditer(r"\n(?:mutable\s+)?struct\s+(\w+)(.*?)\nend", src, re.S):
+        fields = []
+        for ln in m.group(2).split("\n"):
+            for f in ln.split(";"):
+                f = f.strip()
+                if "::" in f:
+                    nm, ty = f.split("::", 1)
+                    fields.append((nm.strip(), ty.strip()))
+        structs[m.group(1)] = fields
+    consts = {m.group(1): m.group(2).strip() for m in re.finditer(r"\nconst\s+(\w+)\s*=\s*([^\n]+)", src)}
+    return raw, src, calls, structs, consts
+
+
+# C type -> Julia types that carry it through ccall
+_ARG = {
+    "int": {"Cint"}, "size_t": {"Csize_t"}, "double": {"Float64", "Cdouble"},
+    "const char*": {"Cstring"}, "char*": {"Ptr{UInt8}"},
+    "const double*": {"Ptr{Float64}"}, "double*": {"Ptr{Float64}"},
+    "int*": {"Ptr{Cint}", "Ref{Cint}"}, "long long*": {"Ptr{Clonglong}", "Ref{Clonglong}"},
+    "br_mech*": {"Ptr{Cvoid}"}, "const br_mech*": {"Ptr{Cvoid}"},
+    "br_mech**": {"Ref{Ptr{Cvoid}}", "Ptr{Ptr{Cvoid}}"}, "br_mech* const*": {"Ptr{Ptr{Cvoid}}"},
+    "br_host_mech*": {"Ptr{Cvoid}"}, "const br_host_mech*": {"Ptr{Cvoid}"},
+    "br_host_mech**": {"Ref{Ptr{Cvoid}}", "Ptr{Ptr{Cvoid}}"},
+    "const br_mech_desc*": {"Ref{BrMechDesc}", "Ptr{BrMechDesc}"}, "br_mech_desc*": {"Ref{BrMechDesc}"},
+    "const br_opts*": {"Ref{BrOpts}", "Ptr{BrOpts}"},
+    "br_stats*": {"Ptr{Float64}"},   # [NSTAT x N] Float64: br_stats is BR_NSTAT doubles
+    "br_batch_input*": {"Ref{BrBatchInput}"}, "void*": {"Ptr{Cvoid}"},
+}
+_ARG = {k.replace(" ", ""): v for k, v in _ARG.items()}     # compared with all blanks removed
+_RET = {"int": "Cint", "constchar*": "Cstring"}
+# C struct field type -> Julia field type
+_FIELD = {"int": "Cint", "double": "Float64", "constdouble*": "Ptr{Float64}", "constint*": "Ptr{Cint}",
+          "double*": "Ptr{Float64}", "char": "UInt8"}
+_CSTRUCT_FOR = {"BrMechDesc": "br_mech_desc", "BrOpts": "br_opts", "BrBatchInput": "br_batch_input"}
+
+
+def _jl_field_type(ctype, dims, consts):
+    t = _FIELD[ctype]
+    for d in reversed(dims):
+        t = f"NTuple{{{d},{t}}}"
+    return t
+
+
+def test_julia_ccalls_match_header():
+    _, protos = _header()[1:]
+    _, _, calls, _, _ = _julia()
+    assert len(calls) >= 15, len(calls)
+    for sym, ret, types, nargs in calls:
+        assert sym in protos, f"{sym}: not declared in include/brhip.h"
+        cret, cargs = protos[sym]
+        assert _RET[cret] == ret, (sym, cret, ret)
+        assert len(types) == len(cargs), (sym, types, cargs)
+        assert nargs == len(cargs), (sym, "argument count", nargs, len(cargs))
+        for k, (ct, jt) in enumerate(zip(cargs, types)):
+            assert ct in _ARG, (sym, k, ct)
+            assert jt in _ARG[ct], f"{sym} argument {k}: C {ct!r} bound as Julia {jt!r}"
+
+
+def test_julia_structs_match_header():
+    defines, structs, _ = _header()
+    _, _, _, jstructs, consts = _julia()
+    for jname, cname in _CSTRUCT_FOR.items():
+        cf, jf = structs[cname], jstructs[jname]
+        assert [n for n, _, _ in cf] == [n for n, _ in jf], (jname, [n for n, _, _ in cf], [n for n, _ in jf])
+        for (n, ct, dims), (_, jt) in zip(cf, jf):
+            dims = [{"BR_BATCH_MAXCOMP": "BATCH_MAXCOMP"}.get(d, d) for d in dims]
+            assert _jl_field_type(ct, dims, consts) == jt.replace(" ", ""), (jname, n, ct, dims, jt)
+    assert consts["BATCH_MAXCOMP"] == defines["BR_BATCH_MAXCOMP"]
+
+
+def test_julia_constants_and_stats_rows():
+    defines, structs, _ = _header()
+    raw, src, _, _, consts = _julia()
+    assert int(consts["NSTAT"].split()[0]) == int(defines["BR_NSTAT"]) == len(structs["br_stats"])
+    m = re.search(r"const STAT_FIELDS = \((.*?)\)\n", src, re.S)
+    names = [t.strip().lstrip(":") for t in m.group(1).replace("\n", " ").split(",") if t.strip()]
+    assert names == [n for n, _, _ in structs["br_stats"]]
+    for c in ("KC_UNIT_SLIP", "FALLOFF_XM", "DOC_COVG", "TROE_C4"):
+        assert re.search(rf"Cint\({defines['BR_CONV_' + c]}\)", consts["CONV_" + c]), c
+    # status row used for the retcode: stats[8, ...] = br_stats.status (1-based)
+    assert [n for n, _, _ in structs["br_stats"]].index("status") + 1 == 8
+    assert "stats[8, 1]" in src
+
+
+def test_ctypes_mirror_matches_header():
+    import ctypes as C
+    import _pkgload
+    pkg = _pkgload.load()
+    L = pkg._lib
+    _, structs, protos = _header()
+    ctmap = {"int": C.c_int, "double": C.c_double, "constdouble*": L.dp, "double*": L.dp, "constint*": L.ip}
+    for py, cname in ((L.MechDesc, "br_mech_desc"), (L.Opts, "br_opts"), (L.BatchInput, "br_batch_input")):
+        cf = structs[cname]
+        assert [n for n, _, _ in cf] == [f[0] for f in py._fields_], cname
+        for (n, ct, dims), (_, pt) in zip(cf, py._fields_):
+            if dims:
+                assert issubclass(pt, C.Array), (cname, n)
+            else:
+                assert pt == ctmap[ct], (cname, n, ct, pt)
+    for sym in L.EXPORTS:
+        assert sym in protos, sym
+    for sym in protos:
+        assert sym in L.EXPORTS, f"{sym} declared in brhip.h but not bound by _lib.py"
+
+
+def test_julia_public_methods_cover_the_reference():
+    """The reference's three public methods (src/BatchReactor.jl:51-54 udf, :67-70 file-driven, :86
+    programmatic with chem / thermo_obj / md), each with the reference's keywords, plus the selector of
+    the reference's own Jacobian (CVODE_BDF's DQ Jacobian, :140/:204) on the solver options."""
+    _, src, _, _, _ = _julia()
+    sigs = [re.sub(r"\s+", " ", m.group(1)) for m in re.finditer(r"\nfunction batch_reactor\((.*?)\)\n", src, re.S)]
+    assert len(sigs) == 3, sigs
+    udf = [s for s in sigs if "::Function" in s]
+    assert udf and "sens" in udf[0], sigs
+    filed = [s for s in sigs if "lib_dir::AbstractString;" in s]
+    assert filed and all(k in filed[0] for k in ("sens", "surfchem", "gaschem", "dq_jacobian")), filed
+    prog = [s for s in sigs if "inlet_comp" in s]
+    assert prog and all(k in prog[0] for k in ("Asv", "chem", "thermo_obj", "md")), prog
+    m = re.search(r"\nBrOpts\(;(.*?)\) =", src, re.S)
+    assert m and "dq_jacobian" in m.group(1)
+    assert re.search(r"struct UserDefinedState", src) and re.search(r"struct Chemistry", src)
+
+
+def test_integration_md_method_list_matches_the_binding():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    _, src, _, _, _ = _julia()
+    assert "user_defined" in doc or "udf" in doc
+    for kw in ("chem", "thermo_obj", "dq_jacobian"):
+        assert kw in doc, kw
+    assert src.count("\nfunction batch_reactor(") == 3
+
+
+if __name__ == "__main__":
+    pytest.main([__file__, "-q"])
