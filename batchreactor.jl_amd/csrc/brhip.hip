@@ -24,6 +24,7 @@
 #define BR_PHASE_CLOCKS 0   // per-phase shader-clock counters in br_stats (diagnostic build: libbrhip_diag.so)
 #endif
 #include "brhip_device.hpp"
+#include "brhip_lug.hpp"   // the lane-grid LU (BR_LU_GRID)
 // Diagnostic-only instruction-count experiments (scripts/micro/exp_hooks.hpp: a phase run twice,
 // extra VALU or memory work per Newton iteration) attach at these points of k_integrate; the
 // product build leaves them empty.
@@ -1077,6 +1078,14 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane,
 // lu_factor_mf stays built and tested (br_debug_lu_solve_mf).
 #define BR_LU_MFMA 0
 #endif
+// CPL = 1, NMAX 32 / 56 / 64: 1 = the 4 x 16 lane-grid LU (lu_factor_g, brhip_lug.hpp: pivot-row
+// values broadcast by the FMA's DPP modifier instead of a v_readlane pair per element, multipliers
+// exchanged through LDS; bit-identical factors, GPU suite and bitcmp); 0 (default) = the row-per-lane
+// lu_factor. Measured in-engine (round 5, profiles/r05_lu_ab.json): see DESIGN.md section 5
+#ifndef BR_LU_GRID
+#define BR_LU_GRID 0
+#endif
+__host__ __device__ constexpr bool lu_grid(int nmax) { return BR_LU_GRID && (nmax == 32 || nmax == 56 || nmax == 64); }
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
@@ -1283,6 +1292,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
                 lu_fail = lu_factor_mf<NMAX>(Jsave, LUsave, (LDSd*)S.sp, ud(C->gamma), n, lane, perm[0]);
                 wave_sync();
                 if (lane == 0) S.sp[Lay<CPL>::ONE] = 1.0;
+            } else if constexpr (CPL == 1 && lu_grid(NMAX)) {
+                lu_fail = lu_factor_g<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm[0]);
             } else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
@@ -2315,8 +2326,9 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     // search + gather path), the second in the first one's pivot order (every pivot on its own lane:
     // the factors come out in step order, no gather); the solve uses the second one's factors
     int perm = lane;
-    auto factor = [&]() {
+    auto factor = [&]() __attribute__((always_inline)) {
         if constexpr (MF) return lu_factor_mf<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
+        else if constexpr (lu_grid(NMAX)) return lu_factor_g<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
         else return lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
     };
     int f = factor();
@@ -2485,6 +2497,22 @@ extern "C" int br_debug_lu_solve_mf(int N, int n, const double* J, const double*
     HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));
     return 0;
 }
+
+#if BR_LUG_STATS
+// diagnostic build only (not declared in brhip.h): read and reset the grid-LU event counts
+// (brhip_lug.hpp: factorizations, steps, pivot handler calls, ties, interchanges, sum of their steps)
+extern "C" int br_debug_lug_stats(double* out8) {
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(brhip::g_lug_stats), sizeof v) != hipSuccess) return -1;
+    for (int i = 0; i < 8; ++i) out8[i] = (double)v[i];
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(brhip::g_lug_stats), z, sizeof z) != hipSuccess) return -1;
+    return 0;
+}
+extern "C" int br_debug_lug_dump(unsigned long long* out2048) {
+    return hipMemcpyFromSymbol(out2048, HIP_SYMBOL(brhip::g_lug_dump), 256 * 8 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if BR_PHASE_CLOCKS
 // diagnostic build only (not declared in brhip.h): read and reset the 16 sub-phase clock sums

@@ -906,6 +906,8 @@ typedef struct {
     /* last-RHS state for save_data semantics */
     double p_last, x_last[MAXSP], th_last[MAXSP];
     double tstop;
+    int lu_map[MAXSP];      /* step -> original row of the previous factorization (diagnostic) */
+    int lu_nmap;
 } cv_t;
 
 static double wrms(const cv_t* cv, const double* x) {
@@ -972,6 +974,59 @@ static void dq_jac(cv_t* cv, const double* y, const double* fy, double* Jc /* co
     free(ft);
 }
 
+/* diagnostic (scripts/lu_order_stats.py; off unless orc_lu_diag(1)): how often a factorization's
+ * pivot sequence differs from the previous factorization's of the same integration, i.e. how often
+ * an engine that loads the rows in the previous pivot order meets a pivot off its step's position,
+ * and how many such steps (row interchanges needed, denseGETRF on the reordered rows) */
+static _Thread_local int g_lu_diag = 0;
+static _Thread_local long g_lu_stat[8];   /* factorizations, deviating ones, steps, interchanges,
+                                              sum of interchange steps k, sum of k - (k >= 32 ? 32 : 0),
+                                              first factorization's interchanges, steps whose column max
+                                              shares its high word with another candidate */
+void orc_lu_diag(int on) { g_lu_diag = on; for (int i = 0; i < 8; ++i) g_lu_stat[i] = 0; }
+void orc_lu_stats(long* out8) { for (int i = 0; i < 8; ++i) out8[i] = g_lu_stat[i]; }
+static void lu_order_diag(cv_t* cv) {
+    int n = cv->n;
+    double* B = (double*)malloc(sizeof(double) * (size_t)n * n);
+    int* pv = (int*)malloc(sizeof(int) * (size_t)n);
+    int map[MAXSP];
+    if (cv->lu_nmap != n) { for (int i = 0; i < n; ++i) cv->lu_map[i] = i; cv->lu_nmap = n; }
+    /* rows in the previous pivot order: position s holds original row lu_map[s] */
+    for (int j = 0; j < n; ++j) for (int s = 0; s < n; ++s) B[(size_t)j * n + s] = cv->A[(size_t)j * n + cv->lu_map[s]];
+    for (int s = 0; s < n; ++s) map[s] = cv->lu_map[s];
+    int sw = 0;
+    {   /* hi-word ties of the column max among the candidates, in the reordered matrix (a copy) */
+        double* Cc = (double*)malloc(sizeof(double) * (size_t)n * n);
+        int* pc = (int*)malloc(sizeof(int) * (size_t)n);
+        memcpy(Cc, B, sizeof(double) * (size_t)n * n);
+        for (int k = 0; k < n; ++k) {
+            double* ck = Cc + (size_t)k * n;
+            int l = k;
+            for (int i = k + 1; i < n; ++i) if (fabs(ck[i]) > fabs(ck[l])) l = i;
+            unsigned long long bl; double al = fabs(ck[l]); memcpy(&bl, &al, 8);
+            int cnt = 0;
+            for (int i = k; i < n; ++i) { double ai = fabs(ck[i]); unsigned long long bi; memcpy(&bi, &ai, 8); if ((bi >> 32) == (bl >> 32)) ++cnt; }
+            if (cnt > 1) g_lu_stat[7]++;
+            if (ck[l] == 0.0) break;
+            if (l != k) for (int i = 0; i < n; ++i) { double t = Cc[(size_t)i * n + l]; Cc[(size_t)i * n + l] = Cc[(size_t)i * n + k]; Cc[(size_t)i * n + k] = t; }
+            double mult = 1.0 / ck[k];
+            for (int i = k + 1; i < n; ++i) ck[i] *= mult;
+            for (int j = k + 1; j < n; ++j) { double* cj = Cc + (size_t)j * n; double akj = cj[k]; if (akj != 0.0) for (int i = k + 1; i < n; ++i) cj[i] -= akj * ck[i]; }
+        }
+        free(Cc); free(pc);
+    }
+    if (getrf(B, n, pv) == 0) {
+        for (int k = 0; k < n; ++k) if (pv[k] != k) {
+            int t = map[k]; map[k] = map[pv[k]]; map[pv[k]] = t; ++sw;
+            g_lu_stat[4] += k; g_lu_stat[5] += k >= 32 ? k - 32 : k;
+        }
+    }
+    if (g_lu_stat[0] == 0) g_lu_stat[6] = sw;
+    g_lu_stat[0]++; g_lu_stat[1] += sw > 0; g_lu_stat[2] += n; g_lu_stat[3] += sw;
+    for (int s = 0; s < n; ++s) cv->lu_map[s] = map[s];
+    free(B); free(pv);
+}
+
 /* cvLsSetup: build A = I - gamma*J (maybe reusing savedJ) and factor */
 static int ls_setup(cv_t* cv, int convfail, const double* ypred, const double* fpred) {
     int n = cv->n;
@@ -995,6 +1050,7 @@ static int ls_setup(cv_t* cv, int convfail, const double* ypred, const double* f
     }
     for (size_t i = 0; i < (size_t)n * n; ++i) cv->A[i] *= -cv->gamma;
     for (int i = 0; i < n; ++i) cv->A[(size_t)i * n + i] += 1.0;
+    if (g_lu_diag) lu_order_diag(cv);
     return getrf(cv->A, n, cv->piv);
 }
 

@@ -110,6 +110,13 @@ int  orc_integrate_out(const orc_mech* m, double T, double Asv, double* u, doubl
                        orc_stats* st, int nout, const double* tout, double* yout);
 /* diagnostic: perturb every rate of progress by a relative +-eps (0 = off; not thread-safe) */
 void orc_set_rop_jitter(double eps);
+/* diagnostic: pivot-order statistics of the factorizations (this thread; orc_lu_diag(1) resets and
+ * enables): out4 = factorizations, those whose pivot order differs from the previous one's, steps,
+ * row interchanges needed when the rows are loaded in the previous pivot order, sum of their steps,
+ * the same within a 32-column panel, the first factorization's interchanges, steps whose column max shares
+ * its high word with another candidate */
+void orc_lu_diag(int on);
+void orc_lu_stats(long* out8);
 /* ensemble (OpenMP over reactors): u[N][n] row per reactor */
 int  orc_integrate_batch(const orc_mech* m, int N, const double* T, const double* Asv,
                          double* u, const double* tf, const orc_opts* o, orc_stats* st,

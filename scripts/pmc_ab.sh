@@ -11,10 +11,12 @@ P2="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_V
 P3="SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_ANY"
 P4="FETCH_SIZE"
 P5="WRITE_SIZE"
+P6="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE"
+P7="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_IFETCH"
+# PASSES: which of the passes above to run (default 1..5)
 for L in ${LIBS}; do
-  i=0
-  for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
-    i=$((i+1))
+  for i in ${PASSES:-1 2 3 4 5}; do
+    eval P=\$P$i
     BRHIP_LIB=$PWD/batchreactor.jl_amd/$L timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmcab_${L}_$i -o run -- python3 bench.py $A > gpurun_out/pmcab_${L}_$i.log 2>&1 || { echo "pass $i of $L failed"; tail -3 gpurun_out/pmcab_${L}_$i.log; }
   done
 done
