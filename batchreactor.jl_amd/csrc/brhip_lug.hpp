@@ -256,9 +256,7 @@ __device__ __forceinline__ void lug_elim(LugState<NMAX>& S, int k, int c, int r,
     constexpr int rk = I & 3, qk = I >> 2;
     auto& a = S.a;
     const double piv = bcast(a[0][qk], 16 * rk + I);
-    // rinv in VGPRs (it meets per-lane values in selects; a uniform SGPR copy of it next to them made
-    // the instruction selector build illegal VGPR -> SGPR register sequences)
-    const double rinv = g_opq(1.0 / piv);
+    const double rinv = 1.0 / piv;
     double l[TS];
     l[0] = (c > I) ? a[0][qk] * rinv : 0.0;
 #pragma unroll
@@ -277,7 +275,7 @@ __device__ __forceinline__ void lug_elim(LugState<NMAX>& S, int k, int c, int r,
     wave_sync();
     double lb[TS];
 #pragma unroll
-    for (int t = 0; t < TS; ++t) lb[t] = g_opq(xch[TS * c + t]);
+    for (int t = 0; t < TS; ++t) lb[t] = xch[TS * c + t];
     wave_sync();
     asm volatile("s_nop 1");
     // rank-1 update of the live registers: slots TS-1..1 first (they read the pivot-row values of

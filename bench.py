@@ -30,6 +30,8 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 dense (vector; the fp64 matrix rate is the same)
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_ACHIEVABLE_GBS = 6300.0   # achievable HBM read rate (MI355X_MICROARCH.md, HBM section)
+DQ_SAMPLE = 2000          # reactors of the DQ-Jacobian parity windows (cpu_baseline leg)
 CONFIGS = {
     "gri": dict(gas="grimech.dat", surf=None, n=100000, tf=10.0,
                 name="C3 test/batch_ch4 GRI-Mech 3.0 CH4/O2/N2 ensemble (53 species, 325 reactions)"),
@@ -141,20 +143,22 @@ def main():
     # algorithmic HBM bytes per launch: inputs (T, Asv, tf, u0[n]) read, u[n] + stats written
     alg_bytes = N * 8.0 * ((3 + mech.n) + (mech.n + pkg._lib.NSTAT))
 
-    # measured memory-side bytes per reactor of this kernel at this HEAD (rocprofv3 FETCH_SIZE x2
-    # + WRITE_SIZE passes, scripts/pmc_traffic.py -> profiles/r04_traffic_<config>.json)
-    traffic, traffic_src = None, None
-    tpath = None
-    for rnd in ("r04", "r03", "r02"):   # the newest round's summary
-        cand = os.path.join(ROOT, "profiles", f"{rnd}_traffic_{args.config}.json")
-        if os.path.exists(cand):
-            tpath = cand
-            break
-    if tpath:
-        with open(tpath) as fh:
-            tj = json.load(fh)
+    # measured L2-fabric-side bytes per reactor of this kernel (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE
+    # passes, scripts/pmc_traffic.py -> profiles/rNN_traffic_<config>.json); Infinity-Cache hits are
+    # counted there, so it is not HBM traffic. The DRAM-destined view and the HBM bound come from
+    # scripts/pmc_dram.sh -> profiles/rNN_dram_<config>.json.
+    def newest(kind):
+        for rnd in ("r05", "r04", "r03", "r02"):
+            cand = os.path.join(ROOT, "profiles", f"{rnd}_{kind}_{args.config}.json")
+            if os.path.exists(cand):
+                with open(cand) as fh:
+                    return json.load(fh), os.path.relpath(cand, ROOT)
+        return None, None
+    traffic = None
+    tj, traffic_src = newest("traffic")
+    if tj:
         traffic = tj["bytes_per_reactor"] * N
-        traffic_src = os.path.relpath(tpath, ROOT)
+    dj, dram_src = newest("dram")
 
     gather_ms = None
     if world > 1:   # the gather alone (it is also inside every timed step above)
@@ -183,15 +187,31 @@ def main():
         kernel_s = kernel_ms * 1e-3
         roof = {"bound": "fp64 valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                "traffic_unit": "B per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, per reactor x N)",
+                "traffic_unit": "B per launch at the L2 memory side (PMC FETCH_SIZE x2 + WRITE_SIZE, per reactor x N; "
+                                "Infinity-Cache hits included, not HBM bytes: see hbm.dram_*)",
                 "traffic_source": traffic_src, "kernel": eng.kernel_name, "kernel_ms": kernel_ms,
                 "launch": eng.launch_info,
                 "algorithmic_flop_per_launch": flops,
                 "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
                         "algorithmic_GBs": alg_bytes / kernel_s / 1e9,
-                        "measured_GBs": (traffic / kernel_s / 1e9) if traffic else None,
                         "peak_GBs": HBM_PEAK_GBS,
-                        "frac_measured": (traffic / kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None}}
+                        # everything the L2 sent to the fabric: Infinity-Cache (MALL) hits included
+                        "l2_fabric_GBs": (traffic / kernel_s / 1e9) if traffic else None,
+                        "l2_fabric_frac_of_hbm_peak": (traffic / kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                        "l2_fabric_source": traffic_src}}
+        if dj:
+            dram_b = dj["dram_destined"]["bytes_per_reactor"] * N
+            roof["hbm"].update({
+                # requests addressed to DRAM, counted before the Infinity Cache serves them (no gfx950
+                # counter separates MALL hits), so an upper bound of HBM bytes
+                "dram_destined_GBs": dram_b / kernel_s / 1e9,
+                "dram_destined_frac_of_hbm_peak": dram_b / kernel_s / 1e9 / HBM_PEAK_GBS,
+                # HBM cannot have moved more than its achievable rate x this kernel's time: the rest of
+                # the fabric-side bytes were Infinity-Cache hits
+                "hbm_achievable_GBs": HBM_ACHIEVABLE_GBS,
+                "min_infinity_cache_share": (max(0.0, 1.0 - HBM_ACHIEVABLE_GBS * 1e9 * kernel_s / traffic)
+                                             if traffic else None),
+                "dram_source": dram_src})
         if phases:
             # the north_star's rate+Jacobian figure: their FLOPs over the kernel time spent in them
             f = ensemble.flop_model(mech)
@@ -341,6 +361,25 @@ def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds, eng):
             "max": W.max(0).tolist(), "p99": np.percentile(W, 99, axis=0).tolist(),
             "median": np.median(W, axis=0).tolist(),
             "frac_within_bounds": float(np.mean(np.all(W <= np.array(bnd[:3]), axis=1)))}
+        # the same windows with CVODE's DQ Jacobian on both sides (the reference's own setting: the
+        # wavefront engine's dq_jacobian path against the oracle's cvLsDenseDQJac), bounded sample
+        if (config, True) in PB.BOUNDS:
+            kd = int(max(1, min(k, DQ_SAMPLE, 0.25 * seconds / max(2.0 * per, 1e-6) * threads)))
+            t2 = time.perf_counter()
+            _, stq, _, Yq = om.integrate_batch(T[:kd], Asv[:kd], U0[:kd], tf[:kd], analytic_jac=False,
+                                               nthreads=threads, tout=PB.OUT_T)
+            dt2 = time.perf_counter() - t2
+            _, sgq = eng.integrate(T[:kd], Asv[:kd], U0[:kd], tf[:kd], tout=PB.OUT_T, dq_jacobian=True)
+            okq = np.array([s["status"] == 0 for s in stq]) & (sgq["status"] == 0)
+            Wq = np.array([PB.band_errors(sgq["yout"][i], Yq[i], stq[i]["t_ign"]) for i in np.nonzero(okq)[0]])
+            bq = PB.BOUNDS[(config, True)]
+            rel["windows_dq"] = {
+                "metric": rel["windows"]["metric"] + "; both sides with CVODE's difference-quotient Jacobian",
+                "reactors": int(okq.sum()), "failed_either": int((~okq).sum()), "bounds": list(bq[:3]),
+                "max": Wq.max(0).tolist(), "p99": np.percentile(Wq, 99, axis=0).tolist(),
+                "median": np.median(Wq, axis=0).tolist(),
+                "frac_within_bounds": float(np.mean(np.all(Wq <= np.array(bq[:3]), axis=1))),
+                "oracle_s": dt2}
     else:
         rel = None
     return ({"value": k / dt, "unit": "reactors/s", "cores": threads, "kind": "port",
