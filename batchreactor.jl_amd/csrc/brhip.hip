@@ -2092,7 +2092,7 @@ static int integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv
         const int GL = m->grp_gl;
         const int gpb = BR_QWPB * (64 / GL);
         const int blocks = std::max(1, std::min((N + gpb - 1) / gpb, m->grp_blocks));
-        const size_t need = (size_t)blocks * gpb * GL * GL * sizeof(double);
+        const size_t need = (size_t)blocks * gpb * grp::slot_doubles(GL, m->nrg) * sizeof(double);
         if (m->qws_bytes < need) {
             if (m->qws) hipFree(m->qws);
             m->qws = nullptr; m->qws_bytes = 0;

@@ -17,7 +17,15 @@
 // reaction | fod: {k0/kinf, log10 Fcent, c, n} per falloff reaction | skd: k(T) per surface
 // reaction]. Global: the saved Jacobian, GL x GL column-major per group slot. Mechanism tables as for
 // the wavefront engine (LDS image, records with the pad species 64 = conc 1.0).
+// BR_QKD_GLOBAL=1: kd lives in the group's global slot after its saved Jacobian (L2-resident: a
+// few hundred bytes per group), and a gas-only 16-lane species block drops its surface sums (66
+// doubles instead of 82): 2.38 instead of 2.83 KB of LDS per H2/O2 reactor, so four 16-reactor
+// workgroups (16 waves) fit a CU's 160 KB instead of three.
 #pragma once
+
+#ifndef BR_QKD_GLOBAL
+#define BR_QKD_GLOBAL 1
+#endif
 
 namespace grp {
 // species block of a group (doubles): conc[CONC + k], gas production sums ACCW, surface production
@@ -34,12 +42,27 @@ struct GLay {
 constexpr int MAX_SETS = 32;
 __host__ __device__ inline int vbytes(int gl) { return NVEC * gl * 8; }
 __host__ __device__ inline int sp_off(int gl) { return CTL_BYTES + vbytes(gl); }
-__host__ __device__ inline int kd_off(int gl) { return sp_off(gl) + (gl == 16 ? GLay<16>::DOUBLES : GLay<32>::DOUBLES) * 8; }
+// species-block doubles: gas-only 16-lane groups need no surface sums (ACCS) past ONE = 64
+__host__ __device__ inline int sp_doubles(int gl, int nrs) {
+    return gl == 16 ? ((BR_QKD_GLOBAL && nrs == 0) ? 66 : GLay<16>::DOUBLES) : GLay<32>::DOUBLES;
+}
+// kd in LDS (BR_QKD_GLOBAL 0): right after the species block
+__host__ __device__ inline int kd_off(int gl, int nrs) { return sp_off(gl) + sp_doubles(gl, nrs) * 8; }
+__host__ __device__ inline int kd_lds_bytes(int nrg) { return BR_QKD_GLOBAL ? 0 : 16 * nrg; }
+__host__ __device__ inline int fod_off(int gl, int nrg, int nrs) { return kd_off(gl, nrs) + kd_lds_bytes(nrg); }
 __host__ __device__ inline int block_bytes(int gl, int nrg, int nfo, int nrs) {
-    const int b = kd_off(gl) + 16 * nrg + 32 * nfo + 8 * nrs;
+    const int b = fod_off(gl, nrg, nrs) + 32 * nfo + 8 * nrs;
     return (b + 15) / 16 * 16;
 }
+// global doubles per group slot: the saved Jacobian (GL x GL), then kd when BR_QKD_GLOBAL (64-B aligned)
+// (at least 8: the RHS prefetches the pair of reaction 0 even when there are no gas reactions)
+__host__ __device__ inline int slot_doubles(int gl, int nrg) { return gl * gl + (BR_QKD_GLOBAL ? ((2 * nrg + 7) / 8 * 8 > 8 ? (2 * nrg + 7) / 8 * 8 : 8) : 0); }
 }  // namespace grp
+#if BR_QKD_GLOBAL
+typedef BR_GLOBAL double QKd;   // {kf, kr} pairs: the group slot in global memory
+#else
+typedef double QKd;
+#endif
 
 // max of a 32-bit value over each 16-lane DPP row (every lane gets its row's max)
 __device__ __forceinline__ unsigned row_umax(unsigned x) {
@@ -96,7 +119,7 @@ __device__ __forceinline__ double group_bcast(double v) {
 // reaction into kd, falloff constants into fod, k(T) per surface reaction into skd; g/RT per gas
 // species in the ACCW slots (scratch)
 template <int GL>
-__device__ __forceinline__ void g_init_tconst(const Tab& tb, double* sp, double* kd, double* fod, double* skd, double T,
+__device__ __forceinline__ void g_init_tconst(const Tab& tb, double* sp, QKd* kd, double* fod, double* skd, double T,
                                               int gl) {
     typedef grp::GLay<GL> L;
     const double lT = log(T);
@@ -155,6 +178,12 @@ __device__ __forceinline__ void g_init_tconst(const Tab& tb, double* sp, double*
         else k = spr[0] * pow(T, spr[1]) * exp(-spr[2] / RT);
         skd[r] = k;
     }
+#if BR_QKD_GLOBAL
+    // the kd stores reach L2 and this CU's L1 is invalidated before any lane reads the slot (it held
+    // the previous reactor's constants), as init_tconst's RXD
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     wave_sync();
 }
 
@@ -162,8 +191,8 @@ __device__ __forceinline__ void g_init_tconst(const Tab& tb, double* sp, double*
 // wavefront engine's order; pad slots read conc[ONE] = 1), the reactant / product concentrations
 // kept for the Jacobian
 template <int GL>
-__device__ __forceinline__ double g_mass_action(const double* sp, const double* kd, uint32_t w0, uint32_t w1, int r,
-                                                double (&cf)[4], double (&cb)[4]) {
+__device__ __forceinline__ double g_mass_action_k(const double* sp, double2 k, uint32_t w0, uint32_t w1,
+                                                  double (&cf)[4], double (&cb)[4]) {
     typedef grp::GLay<GL> L;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -172,7 +201,16 @@ __device__ __forceinline__ double g_mass_action(const double* sp, const double* 
     }
     double Pf = (cf[0] * cf[1]) * cf[2], Pb = (cb[0] * cb[1]) * cb[2];
     if (MF(nu4)) { Pf *= cf[3]; Pb *= cb[3]; }
-    return kd[2 * r] * Pf - kd[2 * r + 1] * Pb;
+    return k.x * Pf - k.y * Pb;
+}
+// {kf, kr} of gas reaction r: one 16-byte load
+__device__ __forceinline__ double2 g_kpair(const QKd* kd, int r) {
+    return make_double2(kd[2 * r], kd[2 * r + 1]);   // (16-B aligned: one dwordx4 load)
+}
+template <int GL>
+__device__ __forceinline__ double g_mass_action(const double* sp, const QKd* kd, uint32_t w0, uint32_t w1, int r,
+                                                double (&cf)[4], double (&cb)[4]) {
+    return g_mass_action_k<GL>(sp, g_kpair(kd, r), w0, w1, cf, cb);
 }
 
 // residual! (src/BatchReactor.jl:312-376) of a group's reactor: du of component gl (gas rates
@@ -180,11 +218,16 @@ __device__ __forceinline__ double g_mass_action(const double* sp, const double* 
 // evaluation to *p_out (save_data semantics). Same arithmetic order as the wavefront engine's rhs()
 // (concentrations, third-body pairing, rate products, falloff, surface coverage factor).
 template <int GL>
-__device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const double* kd, const double* fod, const double* skd,
+__device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const QKd* kd, const double* fod, const double* skd,
                                         double T, double Asv, double Asv_th, double u, int gl, double* p_out) {
     typedef grp::GLay<GL> L;
     const int n = MF(n), ng = MF(ng), nrg = MF(nrg), nrs = MF(nrs), nset = MF(nset);
     const bool gas = gl < ng;
+    // the {kf, kr} pairs of this lane's first two gas reactions, issued before the concentration and
+    // third-body setup so their latency overlaps it (kd is in global memory with BR_QKD_GLOBAL)
+    const double2 kz = make_double2(0.0, 0.0);
+    const double2 kp0 = nrg > 0 ? g_kpair(kd, gl < nrg ? gl : 0) : kz;
+    const double2 kp1 = nrg > GL ? g_kpair(kd, gl + GL < nrg ? gl + GL : 0) : kz;
     const double Mk = tb.molwt[gl];
     const double c = gl < n ? (gas ? u / Mk : u) : 0.0;              // c_k = u_k / M_k; coverages as is
     sp[L::CONC + gl] = c;
@@ -217,13 +260,18 @@ __device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const double*
     double* accw = sp + L::ACCW;
     double* accs = sp + L::ACCS;
     const bool xm = (MF(conv) & 2) != 0;
+    int it = 0;   // (uniform: the pass index)
 #pragma unroll 1
-    for (int r = gl; r < nrg; r += GL) {                               // gas reaction r on lane r mod GL
+    for (int r = gl; r < nrg; r += GL, ++it) {                         // gas reaction r on lane r mod GL
         const auto rr = rx_rec(tb.rx, r);
         const uint4 ra = *reinterpret_cast<const uint4*>(rr.a);
         const uint4 rb = *reinterpret_cast<const uint4*>(rr.b);
         double cf[4], cb[4];
-        double D = g_mass_action<GL>(sp, kd, ra.x, ra.y, r, cf, cb);
+        double2 kp;
+        if (it == 0) kp = kp0;
+        else if (it == 1) kp = kp1;
+        else kp = g_kpair(kd, r);
+        double D = g_mass_action_k<GL>(sp, kp, ra.x, ra.y, cf, cb);
         const int tbk = gi_tb(ra.z);
         if (tbk) {                                                     // as production()'s rate
             const double Mc = sp[L::MC + gi_tbidx(ra.z)];
@@ -276,7 +324,7 @@ __device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const double*
 // evaluates reaction r for its own state); the sparse partials reach their column through scalar
 // compares on the uniform species.
 template <int GL, int NM>
-__device__ __forceinline__ void g_jac(const Tab& tb, const double* sp, const double* kd, const double* fod, int gl,
+__device__ __forceinline__ void g_jac(const Tab& tb, const double* sp, const QKd* kd, const double* fod, int gl,
                                       double (&jr)[NM]) {
     typedef grp::GLay<GL> L;
     const int n = MF(n), ng = MF(ng), nrg = MF(nrg);
@@ -353,10 +401,10 @@ __device__ __forceinline__ void g_jac(const Tab& tb, const double* sp, const dou
 // s (gas rows) or Asv_th sigma_k / Gamma s (surface rows) to the saved-J slot through `jst`. No
 // register tile: the state it needs is the species block of the RHS just evaluated.
 template <int GL, class JST>
-__device__ __forceinline__ void g_jac_cols(const Tab& tb, double* sp, const double* kd, const double* fod, const double* skd,
+__device__ __forceinline__ void g_jac_cols(const Tab& tb, double* sp, const QKd* kd, const double* fod, const double* skd,
                                            double T, double Asv, double Asv_th, int gl, JST&& jst) {
     typedef grp::GLay<GL> L;
-    const int n = MF(n), ng = MF(ng), nrg = MF(nrg);
+    const int n = MF(n), ng = MF(ng), nrg = MF(nrg), nrs = MF(nrs);
     const bool xm = (MF(conv) & 2) != 0;
     const double RT = R_GAS * T, Gs = MF(G);
     const double* conc = sp + L::CONC;
@@ -368,7 +416,7 @@ __device__ __forceinline__ void g_jac_cols(const Tab& tb, double* sp, const doub
 #pragma unroll 1
     for (int j = 0; j < n; ++j) {
         accw[gl] = 0.0;
-        accs[gl] = 0.0;
+        if (nrs) accs[gl] = 0.0;   // (gas-only 16-lane blocks have no surface sums)
         wave_sync();
         const int cb = cp[j], ce = cp[j + 1];
 #pragma unroll 1
@@ -456,7 +504,7 @@ __device__ __forceinline__ void g_jac_cols(const Tab& tb, double* sp, const doub
         wave_sync();
         const bool act = gl < n;
         const double w = act ? accw[gl] : 0.0;
-        const double sf = act ? accs[gl] : 0.0;
+        const double sf = (act && nrs) ? accs[gl] : 0.0;
         double v;
         if (gl < ng) v = (j < ng ? Mk * w / tb.molwt[j] : 0.0) + Mk * Asv * sf;
         else v = Asv_th * tb.sigma[gl] / Gs * sf;
@@ -589,8 +637,10 @@ __device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VT<1, GL>& V, int gl, double (
 #define BR_QWPB 4   // waves per workgroup (16 quad / 8 pair reactors); tables staged once per workgroup
 #endif
 #ifndef BR_QWPE
-#define BR_QWPE 3   // waves per SIMD the register allocation targets for 16-lane groups (<= 168 VGPRs;
-                    // quad H2/O2: 882k reactors/s at 3 vs 693k at 2, round 4)
+#define BR_QWPE 4   // waves per SIMD the register allocation targets for 16-lane groups (<= 128 VGPRs,
+                    // ~128 B/lane spilled). Quad H2/O2: with the LDS block cut to 2.38 KB (BR_QKD_GLOBAL),
+                    // four workgroups fit a CU: 1.100M reactors/s at 4 vs 981k at 3 (round 5); with the
+                    // 2.83 KB block LDS capped it at 12 waves/CU (882k at 3 vs 693k at 2, round 4)
 #endif
 #ifndef BR_QWPE32
 #define BR_QWPE32 3 // ... for 32-lane groups (surface-only Ni/CH4, n = 20: 194.8k reactors/s at 3 (228 B/lane
@@ -615,14 +665,19 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
     LCtl* C = (LCtl*)rbase;
     VA<1, GL> V{(LDbl*)(rbase + CTL_BYTES), gl};
     double* sp = reinterpret_cast<double*>(rbase + grp::sp_off(GL));
-    double* kd = reinterpret_cast<double*>(rbase + grp::kd_off(GL));
-    double* fod = kd + 2 * MF(nrg);
+    double* fod = reinterpret_cast<double*>(rbase + grp::fod_off(GL, MF(nrg), MF(nrs)));
     double* skd = fod + 4 * MF(nfo);
+    const int SD = grp::slot_doubles(GL, MF(nrg));                      // global doubles per group slot
+#if BR_QKD_GLOBAL
+    QKd* kd = launder(Jws) + (size_t)slot * SD + GL * GL;
+#else
+    QKd* kd = reinterpret_cast<double*>(rbase + grp::kd_off(GL, MF(nrs)));
+#endif
     // the group's saved-J slot through a buffer resource: lane offset in a VGPR, the column offset
     // j GL 8 as the instruction's scalar offset (as 64-bit addresses, the columns past 4 KB of a 32-lane
     // slot were materialised per column, hoisted out of the loop and spilled)
     const __amdgpu_buffer_rsrc_t jrs = __builtin_amdgcn_make_buffer_rsrc((void*)launder(Jws), (short)0, 0x7fffffff, 0x00020000);
-    const unsigned jvo = (unsigned)(slot * GL * GL + gl) * 8u;
+    const unsigned jvo = (unsigned)(slot * SD + gl) * 8u;
     auto jst = [&](int j, double v) { __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), jrs, jvo, j * (GL * 8), 0); };
     auto jld = [&](int j) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(jrs, jvo, j * (GL * 8), 0)); };
     const int n = MF(n);
