@@ -1081,11 +1081,18 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane,
 // CPL = 1, NMAX 32 / 56 / 64: 1 = the 4 x 16 lane-grid LU (lu_factor_g, brhip_lug.hpp: pivot-row
 // values broadcast by the FMA's DPP modifier instead of a v_readlane pair per element, multipliers
 // exchanged through LDS; bit-identical factors, GPU suite and bitcmp); 0 (default) = the row-per-lane
-// lu_factor. Measured in-engine (round 5, profiles/r05_lu_ab.json): see DESIGN.md section 5
+// lu_factor. Measured in-engine (round 5, profiles/r05_lu_ab.json): GRI
+// (NMAX 56) -3.1 %, so off there; the surface-only case (NMAX 32) +0.9 %, so BR_LU_GRID32 (default 1)
+// selects it for k_integrate<32> alone
 #ifndef BR_LU_GRID
 #define BR_LU_GRID 0
 #endif
-__host__ __device__ constexpr bool lu_grid(int nmax) { return BR_LU_GRID && (nmax == 32 || nmax == 56 || nmax == 64); }
+#ifndef BR_LU_GRID32
+#define BR_LU_GRID32 1
+#endif
+__host__ __device__ constexpr bool lu_grid(int nmax) {
+    return (BR_LU_GRID && (nmax == 32 || nmax == 56 || nmax == 64)) || (BR_LU_GRID32 && nmax == 32);
+}
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;

@@ -1641,28 +1641,35 @@ __device__ __forceinline__ void dpp_off(double& r, double x, const double (&v)[1
 #ifndef BR_SOLVE_AUX
 #define BR_SOLVE_AUX 0
 #endif
+// Each 8-column chunk is read through its own buffer descriptor: base = the chunk's first column,
+// range = its columns < n. The range check covers the VGPR offset + immediate, not soffset. So the
+// padding columns n..NMAX-1 (zeros) read 0 without a memory access: 3 of 56 columns at GRI's n = 53,
+// 12 of 32 for the surface-only n = 20. No VALU cost; the descriptor is 4 SALU ops per chunk.
 template <bool FWD, int FR>
-__device__ __forceinline__ void tri_load_diag(double (&v)[8], __amdgpu_buffer_rsrc_t rs, int c, unsigned ld8) {
+__device__ __forceinline__ void tri_load_diag(double (&v)[8], const BR_GLOBAL double* wsg, int n, int c, unsigned ld8) {
     // ld8: the lane clamped to FR - 1 (lanes >= FR are never sources; they read row FR - 1)
+    const int live = n - c < 0 ? 0 : (n - c > 8 ? 8 : n - c);
+    const __amdgpu_buffer_rsrc_t rc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(wsg + c * FR), (short)0, live * (FR * 8), 0x00020000);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const unsigned k8 = (unsigned)(c + i) * 8u;
         const unsigned off = FWD ? max(ld8, k8) : min(ld8, k8);
-        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off + i * (FR * 8), c * (FR * 8), BR_SOLVE_AUX));
+        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, off + i * (FR * 8), 0, BR_SOLVE_AUX));
     }
 }
 // block T of a sweep (blocks of 16 columns, the last one NMAX % 16 wide if that is not 0),
 // factor loads one block ahead; x64 = 64 doubles of LDS scratch
 template <bool FWD, int NMAX, int T>
-__device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigned lane8, unsigned ld8, double& r,
+__device__ __forceinline__ void tri_block_dpp(const BR_GLOBAL double* wsg, int n, unsigned lane8, unsigned ld8, double& r,
                                               LDSd* x64, double (&v)[2][16]) {
     constexpr int NB = (NMAX + 15) / 16;
     if constexpr (T < NB) {
         constexpr int B = FWD ? T : NB - 1 - T;            // block = DPP row
         constexpr int CW = (16 * B + 16 > NMAX) ? NMAX - 16 * B : 16;
         auto load = [&](double (&d)[16], int blk) {
-            tri_load_diag<FWD, NMAX>(*reinterpret_cast<double(*)[8]>(&d[0]), rs, 16 * blk, ld8);
-            if (16 * blk + 8 < NMAX) tri_load_diag<FWD, NMAX>(*reinterpret_cast<double(*)[8]>(&d[8]), rs, 16 * blk + 8, ld8);
+            tri_load_diag<FWD, NMAX>(*reinterpret_cast<double(*)[8]>(&d[0]), wsg, n, 16 * blk, ld8);
+            if (16 * blk + 8 < NMAX) tri_load_diag<FWD, NMAX>(*reinterpret_cast<double(*)[8]>(&d[8]), wsg, n, 16 * blk + 8, ld8);
         };
         if constexpr (T == 0) load(v[0], B);
         __builtin_amdgcn_sched_barrier(0);
@@ -1679,13 +1686,13 @@ __device__ __forceinline__ void tri_block_dpp(__amdgpu_buffer_rsrc_t rs, unsigne
             dpp_off<FWD, CW, ROWS, 0>(r, x, f);
             wave_sync();
         }
-        tri_block_dpp<FWD, NMAX, T + 1>(rs, lane8, ld8, r, x64, v);
+        tri_block_dpp<FWD, NMAX, T + 1>(wsg, n, lane8, ld8, r, x64, v);
     }
 }
 template <bool FWD, int NMAX>
-__device__ __forceinline__ void tri_sweep_dpp(__amdgpu_buffer_rsrc_t rs, int lane, double& r, LDSd* x64) {
+__device__ __forceinline__ void tri_sweep_dpp(const BR_GLOBAL double* wsg, int n, int lane, double& r, LDSd* x64) {
     double v[2][16];
-    tri_block_dpp<FWD, NMAX, 0>(rs, (unsigned)lane * 8u, (unsigned)min(lane, NMAX - 1) * 8u, r, x64, v);
+    tri_block_dpp<FWD, NMAX, 0>(wsg, n, (unsigned)lane * 8u, (unsigned)min(lane, NMAX - 1) * 8u, r, x64, v);
     asm volatile("s_nop 1");
 }
 
@@ -1707,9 +1714,10 @@ __device__ __forceinline__ double lu_solve(const double* __restrict__ ws, int n,
         __builtin_amdgcn_make_buffer_rsrc((void*)wsg, (short)0, (NMAX * NMAX + WAVE) * 8, 0x00020000);
     const double dinv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * NMAX * 8, 0));
     double r = lane_pull((lane < n) ? b : 0.0, perm);   // P b
-    tri_sweep_dpp<true, NMAX>(rs, lane, r, x16);
+    const int nu = __builtin_amdgcn_readfirstlane(n);
+    tri_sweep_dpp<true, NMAX>(wsg, nu, lane, r, x16);
     r *= dinv;
-    tri_sweep_dpp<false, NMAX>(rs, lane, r, x16);
+    tri_sweep_dpp<false, NMAX>(wsg, nu, lane, r, x16);
     return (lane < n) ? r : 0.0;
 }
 
@@ -1888,12 +1896,9 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
     const int o1 = min(64 + lane, CR2 - 1);   // (see lu_rl_steps2)
     if (__ballot((lane < n && pstep[0] != lane) || (lane + 64 < n && pstep[1] != lane + 64)) == 0) {
         // every pivot on its own position: M is in step order already; D^-1 in step order
+        // (columns >= n are not zeroed: lu_solve2 never reads them)
         F.D[lane] = dinv[0];
         F.D[o1] = dinv[1];
-        for (int c = n; c < NMAX; ++c) {
-            F.M[c * CR2 + lane] = 0.0;
-            F.M[c * CR2 + o1] = 0.0;
-        }
         perm_io[0] = prow[0];
         perm_io[1] = prow[1];
         return fail;
@@ -1943,8 +1948,10 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
             const int col = t * CH + i;
-            F.M[col * CR2 + lane] = (col < n) ? g[t & 1][0][i] : 0.0;
-            F.M[col * CR2 + o1] = (col < n) ? g[t & 1][1][i] : 0.0;
+            if (col < n) {   // (columns >= n: never read -- the solve's loads of them are out of range)
+                F.M[col * CR2 + lane] = g[t & 1][0][i];
+                F.M[col * CR2 + o1] = g[t & 1][1][i];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -1960,20 +1967,23 @@ __device__ __forceinline__ int lu_factor2(const double* __restrict__ J_, double*
 // Factor loads: diagonal redirect (the step-ordered matrix is 0 at (k, k) and in every row >= n;
 // first-half rows use max/min(row, k); second-half rows that cannot update are sent to k
 // (backward) or, forward, clamped into the 128-B line of rows 64..79, whose rows >= n are zero).
-template <bool FWD, int CW>
+// ncol (block 4 only): columns >= ncol (= n) are zero padding; their loads get an out-of-range offset
+// and read 0 without touching memory (4.6 KB of the ~60 KB a solve reads at n = 66)
+template <bool FWD, int CW, bool LIMIT = false>
 __device__ __forceinline__ void tri2_load_blk(double (&v0)[16], double (&v1)[16], __amdgpu_buffer_rsrc_t rs, int c0,
-                                              unsigned lane8, unsigned hi8, bool want0, bool want1) {
+                                              unsigned lane8, unsigned hi8, bool want0, bool want1, int ncol = 0) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         if (i < CW) {
             const unsigned k8 = (unsigned)(c0 + i) * 8u;
             const int cb = (c0 + i) * CR2 * 8;
+            const bool live = !LIMIT || c0 + i < ncol;
             if (want0) {
-                const unsigned o0 = FWD ? max(lane8, k8) : min(lane8, k8);
+                const unsigned o0 = live ? (FWD ? max(lane8, k8) : min(lane8, k8)) : LU_OOB;
                 v0[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o0, cb, BR_SOLVE_AUX));
             }
             if (want1) {
-                const unsigned o1 = FWD ? min(max(hi8, k8), 79u * 8u) : min(hi8, k8);
+                const unsigned o1 = live ? (FWD ? min(max(hi8, k8), 79u * 8u) : min(hi8, k8)) : LU_OOB;
                 v1[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, cb, BR_SOLVE_AUX));
             }
         }
@@ -1981,7 +1991,7 @@ __device__ __forceinline__ void tri2_load_blk(double (&v0)[16], double (&v1)[16]
 }
 template <int NMAX>
 __device__ __forceinline__ void tri_sweeps2_dpp(__amdgpu_buffer_rsrc_t rs, int lane, double (&r)[2], const double (&dv)[2],
-                                                LDSd* x64) {
+                                                LDSd* x64, int n) {
     static_assert(NMAX > 64 && NMAX <= 72, "CPL = 2 DPP sweeps: 64 < NMAX <= 72");
     constexpr int W1 = NMAX - 64;
     const unsigned lane8 = (unsigned)lane * 8u, hi8 = lane8 + 512u;
@@ -2012,13 +2022,13 @@ __device__ __forceinline__ void tri_sweeps2_dpp(__amdgpu_buffer_rsrc_t rs, int l
     fwd_blk(std::integral_constant<int, 1>{});
     fwd_blk(std::integral_constant<int, 2>{});
     fwd_blk(std::integral_constant<int, 3>{});
-    tri2_load_blk<true, W1>(v0[0], v1, rs, 64, lane8, hi8, false, true);
+    tri2_load_blk<true, W1, true>(v0[0], v1, rs, 64, lane8, hi8, false, true, n);
     dpp_diag<true, W1, 0x1, 0>(r[1], v1);               // block 4
     asm volatile("s_nop 1");
     r[0] *= dv[0];
     r[1] *= dv[1];
     // ---- backward: block 4 (r1) first, then blocks 3..0 (r0)
-    tri2_load_blk<false, W1>(v0[0], v1, rs, 64, lane8, hi8, true, true);
+    tri2_load_blk<false, W1, true>(v0[0], v1, rs, 64, lane8, hi8, true, true, n);
     __builtin_amdgcn_sched_barrier(0);
     tri2_load_blk<false, 16>(v0[1], v1, rs, 48, lane8, hi8, true, false);
     __builtin_amdgcn_sched_barrier(0);
@@ -2074,7 +2084,7 @@ __device__ __forceinline__ void lu_solve2(const double* __restrict__ ws, LDSd* s
     const double dv[2] = {
         __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lane * 8, NMAX * CR2 * 8, 0)),
         __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, min(lane, CR2 - 65) * 8 + 512, NMAX * CR2 * 8, 0))};
-    tri_sweeps2_dpp<NMAX>(rs, lane, r, dv, scr);
+    tri_sweeps2_dpp<NMAX>(rs, lane, r, dv, scr, __builtin_amdgcn_readfirstlane(n));
     b[0] = (lane < n) ? r[0] : 0.0;
     b[1] = (lane + 64 < n) ? r[1] : 0.0;
 }
