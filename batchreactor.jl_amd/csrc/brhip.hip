@@ -113,20 +113,45 @@ enum { V_Z0 = 0, V_ACOR = QMAX + 1, V_EWT, V_TEMP, V_Y, NVEC };   // z0..z5, aco
 // the compiler would hoist out of the integrator loop and keep live (40 VGPRs spilled at 3 waves/
 // SIMD with the previous 72-wide rows and one shared dump row). 6.6 KB per gas+surface reactor.
 constexpr int V1OFF = NVEC * 64;
-__host__ __device__ inline int vec_bytes(int cpl) {
-    return cpl == 2 ? (V1OFF + 8 * (NVEC - 1) + 72 + 64) * 8 : NVEC * WAVE * 8;
+// BR_VS32 = 1: k_integrate<32> (16 < n <= 32) keeps its vectors 32 wide (VS = 32): lanes 32..63 hold
+// no component, read the entry of lane - 32 (a finite value every use of theirs masks: norms, maxima
+// and outputs test component < n) and never store (VProxy below). 2.5 KB less LDS per reactor.
+#ifndef BR_VS32
+#define BR_VS32 1
+#endif
+__host__ __device__ constexpr int vec_stride(int nmax) { return (BR_VS32 && nmax == 32) ? 32 : 64; }
+__host__ __device__ constexpr int nmax_of(int n) { return n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 56 ? 56 : (n <= 64 ? 64 : 72))); }
+__host__ __device__ inline int vec_bytes(int cpl, int vs = 64) {
+    return cpl == 2 ? (V1OFF + 8 * (NVEC - 1) + 72 + 64) * 8 : NVEC * vs * 8;
 }
+typedef __attribute__((address_space(3))) double LDbl;
+// an entry of a VS < 64 vector: loads by every lane, stores by lanes < VS only
+struct VProxy {
+    LDbl* a;
+    bool w;
+    __device__ __forceinline__ operator double() const { return *a; }
+    __device__ __forceinline__ VProxy& operator=(double x) { if (w) *a = x; return *this; }
+    __device__ __forceinline__ VProxy& operator=(const VProxy& o) { return *this = (double)o; }
+    __device__ __forceinline__ VProxy& operator+=(double x) { return *this = (double)*this + x; }
+    __device__ __forceinline__ VProxy& operator-=(double x) { return *this = (double)*this - x; }
+    __device__ __forceinline__ VProxy& operator*=(double x) { return *this = (double)*this * x; }
+};
 // Nordsieck / work vectors in the reactor's LDS block: V.at(vec, s) = component lane + 64 s of
 // vector vec. (Register-resident vectors stored to LDS around each Newton setup measured GRI
 // -1.1 %, surf -11 % in round 2: the extra VGPRs cost occupancy.)
-template <int CPL, int GW = 64>
+template <int CPL, int GW = 64, int VS = GW>
 struct VA {
     typedef __attribute__((address_space(3))) double LD;
     LD* p;
     int lane;
-    __device__ __forceinline__ LD& at(int j, int s) const {
-        if (CPL == 1 || s == 0) return p[j * GW + lane];
-        return p[V1OFF + 8 * j + (lane < 8 ? lane : 72 + lane)];
+    __device__ __forceinline__ decltype(auto) at(int j, int s) const {
+        if constexpr (VS < GW) {
+            static_assert(CPL == 1, "narrow vectors: one component per lane");
+            return VProxy{&p[j * VS + (lane & (VS - 1))], lane < VS};
+        } else {
+            if (CPL == 1 || s == 0) return static_cast<LD&>(p[j * GW + lane]);
+            return static_cast<LD&>(p[V1OFF + 8 * j + (lane < 8 ? lane : 72 + lane)]);
+        }
     }
 };
 template <int CPL, int GW = 64> using VT = VA<CPL, GW>;
@@ -145,10 +170,9 @@ __device__ __forceinline__ void vset(V_& V, int j, int s, double x) {
     for (int jj = 0; jj <= QMAX + 1; ++jj) if (jj == j) V.at(jj, s) = x;
 }
 typedef __attribute__((address_space(3))) Ctl LCtl;
-typedef __attribute__((address_space(3))) double LDbl;
 
 __host__ __device__ inline size_t reactor_bytes(const DevMech& M) {
-    return CTL_BYTES + vec_bytes(M.cpl) + (size_t)M.rblock_bytes;
+    return CTL_BYTES + vec_bytes(M.cpl, vec_stride(nmax_of(M.n))) + (size_t)M.rblock_bytes;
 }
 __host__ __device__ inline size_t wg_lds_bytes(const DevMech& M, int rpb) { return M.img_bytes + rpb * reactor_bytes(M); }
 // per-reactor global workspace (doubles): saved J, LU factors, Jacobian scratch (2 per gas rxn);
@@ -189,7 +213,8 @@ __device__ __forceinline__ WaveCtx wave_ctx(const DevMech& M, char* smem, int rp
     stage_tables(M, smem);
     w.tb = tab_view<CPL>(smem, M);
     w.rbase = smem + M.img_bytes + (size_t)w.wave * reactor_bytes(M);
-    w.R = rview<CPL>(w.rbase + CTL_BYTES + vec_bytes(CPL), M,
+    // (the vector width follows n, as reactor_bytes: the rates / Jacobian kernels run as NMAX 64)
+    w.R = rview<CPL>(w.rbase + CTL_BYTES + vec_bytes(CPL, vec_stride(nmax_of(M.n))), M,
                      launder(ws + (size_t)w.rid * ws_doubles(NMAX, M.nrg) + rxd_ws_off(NMAX, M.nrg)));
     return w;
 }
@@ -323,8 +348,8 @@ __device__ __forceinline__ void track_ignition(LCtl* C, const CtlArgs& a, int la
 }
 // dense output (CVode CV_NORMAL): every tout in (t_{n-1}, t_n] from the Nordsieck array of the step
 // just completed, y(t) = sum_j z_j ((t - tn)/h)^j (CVodeGetDky, k = 0)
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void dense_output(LCtl* C, VT<CPL, GW>& V, const CtlArgs& a, int lane, double tn, double h, int q,
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void dense_output(LCtl* C, VA<CPL, GW, VS>& V, const CtlArgs& a, int lane, double tn, double h, int q,
                                              double tlim) {
     int io = gui<GW>(C->iout);
     while (io < a.nout) {
@@ -452,8 +477,8 @@ __device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4
 }
 
 // Nordsieck rescale of z[1..q] by eta^j; h = hscale*eta
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL, GW>& V, int lane) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void cv_rescale(LCtl* C, VA<CPL, GW, VS>& V, int lane) {
     const int q = gui<GW>(C->q);
     const double eta = ud(C->eta), hscale = ud(C->hscale);
     double f = eta;
@@ -469,8 +494,8 @@ __device__ __forceinline__ void cv_rescale(LCtl* C, VT<CPL, GW>& V, int lane) {
     C->h = h; C->hscale = h;
 }
 // prediction (tn += h, Pascal triangle on z) and its inverse
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL, GW>& V, int lane, const AttemptIn& in) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void cv_predict(LCtl* C, VA<CPL, GW, VS>& V, int lane, const AttemptIn& in) {
     const int q = in.q;
     double tn = in.tn + in.h;
     const double tstop = in.tstop;
@@ -490,8 +515,8 @@ __device__ __forceinline__ void cv_predict(LCtl* C, VT<CPL, GW>& V, int lane, co
         for (int j = 0; j < QMAX; ++j) V.at(j, s) = z[j];
     }
 }
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL, GW>& V, int lane) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void cv_restore(LCtl* C, VA<CPL, GW, VS>& V, int lane) {
     const int q = gui<GW>(C->q);
     C->tn = ud(C->saved_t);
 #pragma unroll
@@ -509,8 +534,8 @@ __device__ __forceinline__ void cv_restore(LCtl* C, VT<CPL, GW>& V, int lane) {
     }
 }
 // cvAdjustOrder for BDF (zn[L] from zn[qmax] = indx_acor on increase)
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void cv_adjust_order(LCtl* C, VT<CPL, GW>& V, int lane, int dq) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void cv_adjust_order(LCtl* C, VA<CPL, GW, VS>& V, int lane, int dq) {
     const int q = gui<GW>(C->q);
     if (q == 2 && dq != 1) return;
     double lv[QMAX + 1] = {0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
@@ -564,8 +589,8 @@ __device__ __forceinline__ void trace_row(LCtl* C, const CtlArgs& a, int lane, i
     }
 }
 // one attempt of cvStep: predict, coefficients, and the Newton iteration's setup decision
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL, GW>& V, int lane, int nflag) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL, GW, VS>& V, int lane, int nflag) {
     const AttemptIn in = load_attempt<GW>(C);
     cv_predict<CPL, GW>(C, V, lane, in);
     double tq4, gamrat;
@@ -583,8 +608,8 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VT<CPL, GW>& V, int lane,
 #pragma unroll
     FOR_S V.at(V_Y, s) = V.at(0, s);   // y = z0
 }
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void begin_step(LCtl* C, VT<CPL, GW>& V, int lane, const CtlArgs& a) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void begin_step(LCtl* C, VA<CPL, GW, VS>& V, int lane, const CtlArgs& a) {
     BR_SUB_T(bt0);
     BR_QMARK(begin_step);
     const double tn = ud(C->tn), hprime = ud(C->hprime), h = ud(C->h);   // read before the V stores
@@ -612,8 +637,8 @@ __device__ __forceinline__ void begin_step(LCtl* C, VT<CPL, GW>& V, int lane, co
 // Controller, part 1: after the RHS value f = F(y) of this lane is known.
 // Returns A_RHS (next y in V[V_Y]), A_SOLVE (delta for the solve returned in *rhs_out),
 // A_SETUP (Jacobian decision in C->newj, then LU and solve), A_DONE.
-template <int CPL, int GW = 64>
-__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VT<CPL, GW>& V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ BR_CTL_INLINE int ctl_post_rhs(LCtl* C, VA<CPL, GW, VS>& V, int lane, const double (&f)[CPL], double (&rhs_out)[CPL]) {
     const CtlArgs a = load_args<GW>(C);
     const int n = a.n;
     C->nfe = gui<GW>(C->nfe) + 1;
@@ -754,8 +779,8 @@ __device__ __forceinline__ double pow_int(double x, int L) {
 // Controller, part 2: after the linear solve (delta = this lane's Newton correction) or after
 // an LU failure (lu_fail != 0). Runs the convergence test, the error test, cvCompleteStep,
 // cvPrepareNextStep and the tstop logic; returns A_RHS (next y in V[V_Y]) or A_DONE.
-template <int CPL, int GW = 64>
-__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, double (&delta)[CPL], int lu_fail) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL, GW, VS>& V, int lane, double (&delta)[CPL], int lu_fail) {
     BR_SUB_T(ps0);
     BR_QMARK(ps_start);
     const CtlArgs a = load_args<GW>(C);
@@ -1016,8 +1041,8 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VT<CPL, GW>& V, int lane, d
 // kernel's single RHS call site (k_integrate: the column index `dqj` routes the result here).
 constexpr double DQ_SRUR = 1.4901161193847656e-08;   // sqrt(UROUND) = 2^-26
 constexpr double DQ_MIN_INC_MULT = 1000.0;
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void dq_begin(LCtl* C, VT<CPL, GW>& V, int lane, const double (&f)[CPL]) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void dq_begin(LCtl* C, VA<CPL, GW, VS>& V, int lane, const double (&f)[CPL]) {
     const int n = gui<GW>(C->a_n);
     double ewt[CPL];
 #pragma unroll
@@ -1029,15 +1054,15 @@ __device__ __forceinline__ void dq_begin(LCtl* C, VT<CPL, GW>& V, int lane, cons
     C->dq_mininc = (fnorm != 0.0) ? (DQ_MIN_INC_MULT * fabs(ud(C->h)) * UROUND * n * fnorm) : 1.0;
 }
 // increment of this lane's components (the one for component j is used by column j)
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void dq_incs(LCtl* C, VT<CPL, GW>& V, int lane, double (&inc)[CPL]) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void dq_incs(LCtl* C, VA<CPL, GW, VS>& V, int lane, double (&inc)[CPL]) {
     const double mininc = ud(C->dq_mininc);
 #pragma unroll
     FOR_S inc[s] = fmax(DQ_SRUR * fabs(V.at(V_Z0, s)), mininc / V.at(V_EWT, s));
 }
 // column j of the saved J from F(y + inc_j e_j) = f (rows as jacobian(): JW per column)
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void dq_column(LCtl* C, VT<CPL, GW>& V, int lane, int j, const double (&f)[CPL], double* Jsave) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void dq_column(LCtl* C, VA<CPL, GW, VS>& V, int lane, int j, const double (&f)[CPL], double* Jsave) {
     constexpr int JW = CPL == 2 ? 80 : 64;
     double inc[CPL];
     dq_incs<CPL, GW>(C, V, lane, inc);
@@ -1053,8 +1078,8 @@ __device__ __forceinline__ void dq_column(LCtl* C, VT<CPL, GW>& V, int lane, int
     C->nfe_dq = gui<GW>(C->nfe_dq) + 1;
 }
 // the Newton right-hand side at the setup point again (cvNlsResidual with f = fy, as ctl_post_rhs)
-template <int CPL, int GW = 64>
-__device__ __forceinline__ void dq_newton_rhs(LCtl* C, VT<CPL, GW>& V, int lane, double (&b)[CPL]) {
+template <int CPL, int GW = 64, int VS = GW>
+__device__ __forceinline__ void dq_newton_rhs(LCtl* C, VA<CPL, GW, VS>& V, int lane, double (&b)[CPL]) {
     const double rl1 = ud(C->rl1), gamma = ud(C->gamma);
 #pragma unroll
     FOR_S b[s] = -((rl1 * V.at(1, s) + V.at(V_ACOR, s)) - gamma * V.at(V_TEMP, s));
@@ -1108,7 +1133,9 @@ __host__ __device__ constexpr int br_maxrpb(int nmax) {
 }
 constexpr size_t LDS_PER_CU = 160 * 1024, LDS_GRANULE = 1280;   // gfx950 (granule: conservative)
 #ifndef BR_WPE32
-#define BR_WPE32 3   // n <= 32 (surface-only): 3 waves/SIMD, 12 waves/CU (LDS allows it; 130k -> 156k/s)
+#define BR_WPE32 5   // n <= 32 (surface-only): 5 waves/SIMD (96 VGPRs, 80 B/lane spilled) -- with the 32-wide
+                     // vectors (BR_VS32) five 4-reactor workgroups fit the LDS: 20 waves/CU, C4 232.8k vs
+                     // 219.7k reactors/s at 16 (round 5); round 2: 3 waves/SIMD, 12 waves/CU, 130k -> 156k/s
 #endif
 // minimum waves per SIMD the register allocator must allow, per instance
 #ifndef BR_WPE72
@@ -1147,8 +1174,8 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
     const Tab& tb = W.tb;
     const size_t roff = (size_t)(W.rbase - smem_raw);
     LCtl* C = (LCtl*)(smem_raw + roff);
-    const VA<CPL> Vm{(LDbl*)(smem_raw + roff + CTL_BYTES), lane};
-    VT<CPL> V = Vm;
+    const VA<CPL, 64, vec_stride(NMAX)> Vm{(LDbl*)(smem_raw + roff + CTL_BYTES), lane};
+    VA<CPL, 64, vec_stride(NMAX)> V = Vm;
     const RView& S = W.R;
     const int n = M.n;
     const double T = Tv[rid];
