@@ -147,7 +147,9 @@ struct VA {
     __device__ __forceinline__ decltype(auto) at(int j, int s) const {
         if constexpr (VS < GW) {
             static_assert(CPL == 1, "narrow vectors: one component per lane");
-            return VProxy{&p[j * VS + (lane & (VS - 1))], lane < VS};
+            // lanes >= VS read a real entry (lane - VS for a power-of-2 width, else the last one)
+            const int li = (VS & (VS - 1)) == 0 ? (lane & (VS - 1)) : (lane < VS ? lane : VS - 1);
+            return VProxy{&p[j * VS + li], lane < VS};
         } else {
             if (CPL == 1 || s == 0) return static_cast<LD&>(p[j * GW + lane]);
             return static_cast<LD&>(p[V1OFF + 8 * j + (lane < 8 ? lane : 72 + lane)]);
@@ -1951,7 +1953,7 @@ int br_mech_create(const br_mech_desc* d, int device, br_mech** out) {
         m->grp_gl = n <= 16 ? 16 : 32;
         m->grp_nm = n <= 9 ? 9 : (n <= 16 ? 16 : (n <= 24 ? 24 : 32));
         const void* gfn = grp_kernel(m->grp_gl, m->grp_nm);
-        m->grp_shmem = (size_t)M.img_bytes + (size_t)BR_QWPB * (64 / m->grp_gl) * grp::block_bytes(m->grp_gl, nrg, M.nfo, nrs);
+        m->grp_shmem = (size_t)M.img_bytes + (size_t)BR_QWPB * (64 / m->grp_gl) * grp::block_bytes(m->grp_gl, m->grp_nm, nrg, M.nfo, nrs);
         int nb = 0;
         if (m->grp_shmem > LDS_PER_CU ||
             hipFuncSetAttribute(gfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->grp_shmem) != hipSuccess ||

@@ -26,6 +26,9 @@
 #ifndef BR_QKD_GLOBAL
 #define BR_QKD_GLOBAL 1
 #endif
+#ifndef BR_QVS
+#define BR_QVS 0
+#endif
 
 namespace grp {
 // species block of a group (doubles): conc[CONC + k], gas production sums ACCW, surface production
@@ -40,18 +43,23 @@ struct GLay {
     static_assert(ONE == Lay<1>::ONE, "pad species");
 };
 constexpr int MAX_SETS = 32;
-__host__ __device__ inline int vbytes(int gl) { return NVEC * gl * 8; }
-__host__ __device__ inline int sp_off(int gl) { return CTL_BYTES + vbytes(gl); }
+// BR_QVS = 1: Nordsieck / work vectors NM wide (the register width >= n: 9 for H2/O2) instead of GL;
+// lanes nm..GL-1 of a group read the last entry and never store (VProxy), 560 B less LDS per H2/O2
+// reactor, enough for five workgroups per CU. Measured (round 5, profiles/r05_h2o2_quad_wpe_ab.json):
+// 1.078M at 4 waves/SIMD and 798k at 5 (96 VGPRs, 284 B/lane spilled) vs 1.096M -- off
+__host__ __device__ constexpr int vstride(int gl, int nm) { return BR_QVS ? nm : gl; }
+__host__ __device__ inline int vbytes(int gl, int nm) { return NVEC * vstride(gl, nm) * 8; }
+__host__ __device__ inline int sp_off(int gl, int nm) { return CTL_BYTES + vbytes(gl, nm); }
 // species-block doubles: gas-only 16-lane groups need no surface sums (ACCS) past ONE = 64
 __host__ __device__ inline int sp_doubles(int gl, int nrs) {
     return gl == 16 ? ((BR_QKD_GLOBAL && nrs == 0) ? 66 : GLay<16>::DOUBLES) : GLay<32>::DOUBLES;
 }
 // kd in LDS (BR_QKD_GLOBAL 0): right after the species block
-__host__ __device__ inline int kd_off(int gl, int nrs) { return sp_off(gl) + sp_doubles(gl, nrs) * 8; }
+__host__ __device__ inline int kd_off(int gl, int nm, int nrs) { return sp_off(gl, nm) + sp_doubles(gl, nrs) * 8; }
 __host__ __device__ inline int kd_lds_bytes(int nrg) { return BR_QKD_GLOBAL ? 0 : 16 * nrg; }
-__host__ __device__ inline int fod_off(int gl, int nrg, int nrs) { return kd_off(gl, nrs) + kd_lds_bytes(nrg); }
-__host__ __device__ inline int block_bytes(int gl, int nrg, int nfo, int nrs) {
-    const int b = fod_off(gl, nrg, nrs) + 32 * nfo + 8 * nrs;
+__host__ __device__ inline int fod_off(int gl, int nm, int nrg, int nrs) { return kd_off(gl, nm, nrs) + kd_lds_bytes(nrg); }
+__host__ __device__ inline int block_bytes(int gl, int nm, int nrg, int nfo, int nrs) {
+    const int b = fod_off(gl, nm, nrg, nrs) + 32 * nfo + 8 * nrs;
     return (b + 15) / 16 * 16;
 }
 // global doubles per group slot: the saved Jacobian (GL x GL), then kd when BR_QKD_GLOBAL (64-B aligned)
@@ -613,12 +621,12 @@ __device__ __forceinline__ double g_solve(const double (&a)[NM], int orig, doubl
 #else
 #define BR_QCTL_ATTR __forceinline__
 #endif
-template <int GL>
-__device__ BR_QCTL_ATTR int g_post_rhs(LCtl* C, VT<1, GL>& V, int gl, const double (&f)[1], double (&b)[1]) {
+template <int GL, int VS>
+__device__ BR_QCTL_ATTR int g_post_rhs(LCtl* C, VA<1, GL, VS>& V, int gl, const double (&f)[1], double (&b)[1]) {
     return ctl_post_rhs<1, GL>(C, V, gl, f, b);
 }
-template <int GL>
-__device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VT<1, GL>& V, int gl, double (&delta)[1], int lu_fail) {
+template <int GL, int VS>
+__device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VA<1, GL, VS>& V, int gl, double (&delta)[1], int lu_fail) {
     return ctl_post_solve<1, GL>(C, V, gl, delta, lu_fail);
 }
 
@@ -660,18 +668,18 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
     const int lane = threadIdx.x & 63, gl = lane & (GL - 1);
     const int grp = (int)(threadIdx.x / GL);                            // group within the workgroup
     const int slot = blockIdx.x * (BR_QWPB * GPW) + grp;                // workspace slot of this group
-    const int RB = grp::block_bytes(GL, MF(nrg), MF(nfo), MF(nrs));
+    const int RB = grp::block_bytes(GL, NM, MF(nrg), MF(nfo), MF(nrs));
     char* rbase = smem_raw + M.img_bytes + (size_t)grp * RB;
     LCtl* C = (LCtl*)rbase;
-    VA<1, GL> V{(LDbl*)(rbase + CTL_BYTES), gl};
-    double* sp = reinterpret_cast<double*>(rbase + grp::sp_off(GL));
-    double* fod = reinterpret_cast<double*>(rbase + grp::fod_off(GL, MF(nrg), MF(nrs)));
+    VA<1, GL, grp::vstride(GL, NM)> V{(LDbl*)(rbase + CTL_BYTES), gl};
+    double* sp = reinterpret_cast<double*>(rbase + grp::sp_off(GL, NM));
+    double* fod = reinterpret_cast<double*>(rbase + grp::fod_off(GL, NM, MF(nrg), MF(nrs)));
     double* skd = fod + 4 * MF(nfo);
     const int SD = grp::slot_doubles(GL, MF(nrg));                      // global doubles per group slot
 #if BR_QKD_GLOBAL
     QKd* kd = launder(Jws) + (size_t)slot * SD + GL * GL;
 #else
-    QKd* kd = reinterpret_cast<double*>(rbase + grp::kd_off(GL, MF(nrs)));
+    QKd* kd = reinterpret_cast<double*>(rbase + grp::kd_off(GL, NM, MF(nrs)));
 #endif
     // the group's saved-J slot through a buffer resource: lane offset in a VGPR, the column offset
     // j GL 8 as the instruction's scalar offset (as 64-bit addresses, the columns past 4 KB of a 32-lane
