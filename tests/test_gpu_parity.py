@@ -269,8 +269,9 @@ def test_ignition_time_and_golden_rows_on_gpu(pkg, gpu, dq):
 
 
 @pytest.mark.parametrize("case,N,dq", [("h2o2", 64, False), ("gri", 32, False), ("surf", 32, False),
-                                      ("gas_surf", 16, False), ("gri", 64, True), ("gas_surf", 32, True)],
-                         ids=["h2o2", "gri", "surf", "gas_surf", "gri-dq", "gas_surf-dq"])
+                                      ("gas_surf", 16, False), ("gri", 64, True), ("gas_surf", 32, True),
+                                      ("surf", 64, True), ("h2o2", 64, True)],
+                         ids=["h2o2", "gri", "surf", "gas_surf", "gri-dq", "gas_surf-dq", "surf-dq", "h2o2-dq"])
 def test_integrate_parity_tight(pkg, orc, gpu, case, N, dq):
     """Tight tolerances (rtol 1e-10, atol 1e-16) on both sides: the two integrations converge to the
     same trajectory, so the end states (tf = 1e-2 s, through ignition for the gas cases) must agree
