@@ -44,7 +44,11 @@ BOUNDS = {
     ("gri", True): (196.0, 3400.0, 50.0, 520.0),
     ("gas_surf", False): (2.1, 1150.0, 16.5, 6.0),
     ("gas_surf", True): (1.9, 1120.0, 9.2, 3.7),
-    ("surf", False): (0.45, 0.45, 0.45, 2.0),
+    # the north star's own bar (1 band = 1e-4 relative): the u0-perturbation spread on 20,000 bench
+    # reactors reaches 0.78 bands (p99 0.20; round 5, profiles/r05_parity_spread_surf.json), so 2x it
+    # would exceed the bar; the round-4 0.45 came from 96 reactors, and the bench's 100,000-reactor
+    # sample shows the same tail on the GPU (max 0.97, p99 0.20)
+    ("surf", False): (1.0, 1.0, 1.0, 2.0),
     # 2x the u0-perturbation spread over the bench sample (65,638 reactors, no rop jitter: the analytic
     # path does not amplify an RHS's rounding the way the DQ Jacobian does; t_ign 1.64 widths)
     ("h2o2", False): (1e-6, 2.1, 5.4, 3.3),
