@@ -296,8 +296,8 @@ __device__ __forceinline__ void lug_elim(LugState<NMAX>& S, int k, int c, int r,
 // 16 unrolled steps of every block, on the state in scratch memory); 0 (default): inline in each
 // step. The inline copies are ~14k instructions (3.6x the I-cache misses of the row-per-lane LU in
 // the engine, r05_lu_ab.json), but the call costs more: micro harness, n = 53, 16 waves/CU, bit-
-// identical: stable pivot order 84.0 vs 69.8 us per LU (the call reshapes the hot path's register
-// allocation), every LU interchanging 27x the row-per-lane time
+// identical: stable pivot order 0.95x the row-per-lane LU's time against 0.84x inline (the call
+// reshapes the hot path's register allocation), every LU interchanging 27x
 #define BR_LUG_OOL 0
 #endif
 
