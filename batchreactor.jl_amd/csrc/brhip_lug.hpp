@@ -291,91 +291,15 @@ __device__ __forceinline__ void lug_elim(LugState<NMAX>& S, int k, int c, int r,
     if (nq > 4) g_for<(qk > 4 ? qk : 4), 8>([&](auto Q) { g_fnma_self<I>(a[0][decltype(Q)::value], lb[0]); });
 }
 
-#ifndef BR_LUG_OOL
-// 1: the cold part of a step whose fast check failed runs out of line (lug_handler, one copy for the
-// 16 unrolled steps of every block, on the state in scratch memory); 0 (default): inline in each
-// step. The inline copies are ~14k instructions (3.6x the I-cache misses of the row-per-lane LU in
-// the engine, r05_lu_ab.json), but the call costs more: micro harness, n = 53, 16 waves/CU, bit-
-// identical: stable pivot order 0.95x the row-per-lane LU's time against 0.84x inline (the call
-// reshapes the hot path's register allocation), every LU interchanging 27x
-#define BR_LUG_OOL 0
-#endif
-
-// exact pivot of local step I (runtime) and, when it is another position p, the in-place interchange of
-// rows k and p: their register rows (staged through LDS), their stored multipliers of columns 0..k-1 and
-// the load order. Returns 1 when singular (no candidate or all zero), else 0.
-template <int NMAX>
-__device__ __forceinline__ int lug_handle(LugState<NMAX>& S, int I, int k, int blk, int c, int r, int lane, int n,
-                                          LDSd* xch, BR_GLOBAL double* wsg) {
-    constexpr int TS = LugState<NMAX>::TS, FR = LugState<NMAX>::FR;
-    const int rk = I & 3, qk = I >> 2;
-    auto& a = S.a;
-    BR_LUG_COUNT(2, 1);
-    int tp = 0;
-    unsigned long long pb = 0;
-    const int p = lug_exact_pivot<NMAX>(S, blk, I, qk, rk, c, n, tp, pb);
-    if (p < 0 || pb == 0ull) return 1;   // no candidate / every candidate 0: singular
-    const int cp = p & 15;
-    if (tp != 0 || cp != I) {
-        BR_LUG_COUNT(4, 1);
-        BR_LUG_COUNT(5, k);
-        const int pos_p = cp + 16 * (blk + tp);
-        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's factor stores are done
-        if (lane < k) {
-            BR_GLOBAL double* col = wsg + (size_t)lane * FR;
-            const double vk = col[k], vpp = col[pos_p];
-            col[k] = vpp;
-            col[pos_p] = vk;
-        }
-        LDSd* stk = xch + 64;
-        LDSd* stp = xch + 96;
-        if (c == I) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) stk[8 * r + q] = a[0][q];
-        }
-        if (c == cp) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                double x = g_opq(a[0][q]);
-#pragma unroll
-                for (int t = 1; t < TS; ++t) x = (tp == t) ? g_opq(a[t][q]) : x;
-                stp[8 * r + q] = x;
-            }
-        }
-        wave_sync();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const double x = stp[8 * r + q];
-            a[0][q] = (c == I) ? x : a[0][q];
-        }
-        // (selects, not branches on tp: stores to a[tp][q] under a branch become stores through a
-        // selected pointer, and the register array is demoted to scratch memory)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const double y = stk[8 * r + q];
-#pragma unroll
-            for (int t = 0; t < TS; ++t) a[t][q] = (tp == t && c == cp) ? y : a[t][q];
-        }
-        wave_sync();
-        lug_swap_order<NMAX>(S, blk, I, tp, cp, c);
-    } else {
-        BR_LUG_COUNT(3, 1);
-    }
-    return 0;
-}
-// out-of-line copy: works on a copy of the state (its address escapes; the caller's state stays in
-// registers), uniform arguments re-marked uniform
-template <int NMAX>
-__device__ __attribute__((noinline)) int lug_handler(LugState<NMAX>* T, int I, int k, int blk, int c, int r, int lane, int n,
-                                                     LDSd* xch, BR_GLOBAL double* wsg) {
-    return lug_handle<NMAX>(*T, g_uni(I), g_uni(k), g_uni(blk), c, r, lane, g_uni(n), xch, wsg);
-}
-
 // one step, in-place interchange variant: on a failed fast check the exact pivot is found and, when it
-// is another position p, rows k and p are exchanged in place. false: singular (fail = k + 1)
+// is another position p, rows k and p are exchanged in place (registers staged through LDS, their
+// stored multipliers of columns 0..k-1, the load order). false: singular (fail = k + 1)
 template <int NMAX, int I>
 __device__ __forceinline__ bool lug_step_ip(LugState<NMAX>& S, int kb, int blk, int c, int r, int lane, int n, int nq, int ns,
                                             __amdgpu_buffer_rsrc_t rs, LDSd* xch, BR_GLOBAL double* wsg, int& fail) {
+    constexpr int TS = LugState<NMAX>::TS, FR = LugState<NMAX>::FR;
+    constexpr int rk = I & 3, qk = I >> 2;
+    auto& a = S.a;
     // opaque per step: the lane tests against this step's constants are made here (hoisted out of
     // the panel loop they become ~60 live lane masks, and the SGPRs spill)
     c = launder_v(c);
@@ -384,16 +308,59 @@ __device__ __forceinline__ bool lug_step_ip(LugState<NMAX>& S, int kb, int blk, 
     ns = g_uni(ns);
     const int k = g_uni(kb) + I;
     if (__builtin_expect(!lug_check<NMAX, I>(S, c), 0)) {
-#if BR_LUG_OOL
-        LugState<NMAX> T = S;
-        const int sing = lug_handler<NMAX>(&T, I, k, g_uni(blk), c, r, lane, n, xch, wsg);
-        S = T;
-#else
-        const int sing = lug_handle<NMAX>(S, I, k, g_uni(blk), c, r, lane, n, xch, wsg);
-#endif
-        if (sing) {
+        BR_LUG_COUNT(2, 1);
+        int tp = 0;
+        unsigned long long pb = 0;
+        const int p = lug_exact_pivot<NMAX>(S, g_uni(blk), I, qk, rk, c, n, tp, pb);
+        if (p < 0 || pb == 0ull) {   // no candidate / every candidate 0: singular
             fail = k + 1;
             return false;
+        }
+        const int cp = p & 15;
+        if (tp != 0 || cp != I) {
+            BR_LUG_COUNT(4, 1);
+            BR_LUG_COUNT(5, k);
+            const int pos_p = cp + 16 * (blk + tp);
+            __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's factor stores are done
+            if (lane < k) {
+                BR_GLOBAL double* col = wsg + (size_t)lane * FR;
+                const double vk = col[k], vpp = col[pos_p];
+                col[k] = vpp;
+                col[pos_p] = vk;
+            }
+            LDSd* stk = xch + 64;
+            LDSd* stp = xch + 96;
+            if (c == I) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) stk[8 * r + q] = a[0][q];
+            }
+            if (c == cp) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    double x = g_opq(a[0][q]);
+#pragma unroll
+                    for (int t = 1; t < TS; ++t) x = (tp == t) ? g_opq(a[t][q]) : x;
+                    stp[8 * r + q] = x;
+                }
+            }
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const double x = stp[8 * r + q];
+                a[0][q] = (c == I) ? x : a[0][q];
+            }
+            // (selects, not branches on tp: stores to a[tp][q] under a branch become stores through a
+            // selected pointer, and the register array is demoted to scratch memory)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const double y = stk[8 * r + q];
+#pragma unroll
+                for (int t = 0; t < TS; ++t) a[t][q] = (tp == t && c == cp) ? y : a[t][q];
+            }
+            wave_sync();
+            lug_swap_order<NMAX>(S, blk, I, tp, cp, c);
+        } else {
+            BR_LUG_COUNT(3, 1);
         }
     }
     lug_elim<NMAX, I>(S, k, c, r, nq, ns, rs, xch);
