@@ -1109,13 +1109,15 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VA<CPL, GW, VS>& V, int l
 // values broadcast by the FMA's DPP modifier instead of a v_readlane pair per element, multipliers
 // exchanged through LDS; bit-identical factors, GPU suite and bitcmp); 0 (default) = the row-per-lane
 // lu_factor. Measured in-engine (round 5, profiles/r05_lu_ab.json): GRI
-// (NMAX 56) -3.1 %, so off there; the surface-only case (NMAX 32) +0.9 %, so BR_LU_GRID32 (default 1)
-// selects it for k_integrate<32> alone
+// (NMAX 56) -3.1 %, so off there; the surface-only case (NMAX 32) +0.3 % in a same-session re-run
+// (BR_LU_GRID32 selects it for k_integrate<32> alone). Off by default: a semantically equivalent
+// refactor of its pivot handler gave wrong surface integrations in the engine while the micro harness
+// stayed bit-identical, so the code is not robust enough for a 0.3 % gain
 #ifndef BR_LU_GRID
 #define BR_LU_GRID 0
 #endif
 #ifndef BR_LU_GRID32
-#define BR_LU_GRID32 1
+#define BR_LU_GRID32 0
 #endif
 __host__ __device__ constexpr bool lu_grid(int nmax) {
     return (BR_LU_GRID && (nmax == 32 || nmax == 56 || nmax == 64)) || (BR_LU_GRID32 && nmax == 32);
