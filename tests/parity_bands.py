@@ -49,6 +49,9 @@ BOUNDS = {
     # would exceed the bar; the round-4 0.45 came from 96 reactors, and the bench's 100,000-reactor
     # sample shows the same tail on the GPU (max 0.97, p99 0.20)
     ("surf", False): (1.0, 1.0, 1.0, 2.0),
+    # 2x the oracle's own DQ spread (rop jitter 4e-16) on 2,000 bench reactors: max 1.97 bands, p99 0.76
+    # (round 5, profiles/r05_dq_spread_surf.json); no ignition
+    ("surf", True): (3.9, 3.9, 3.9, 2.0),
     # 2x the u0-perturbation spread over the bench sample (65,638 reactors, no rop jitter: the analytic
     # path does not amplify an RHS's rounding the way the DQ Jacobian does; t_ign 1.64 widths)
     ("h2o2", False): (1e-6, 2.1, 5.4, 3.3),

@@ -188,8 +188,8 @@ _BANDS = ((0.0, 0.5, 1.0), (0.5, 2.0, 300.0), (2.0, np.inf, 30.0))   # coarse bo
 
 @pytest.mark.parametrize("case,N,dq", [("h2o2", 256, False), ("gri", 64, False), ("surf", 64, False),
                                       ("gas_surf", 32, False), ("h2o2", 256, True), ("gri", 32, True),
-                                      ("gas_surf", 16, True)],
-                         ids=["h2o2", "gri", "surf", "gas_surf", "h2o2-dq", "gri-dq", "gas_surf-dq"])
+                                      ("gas_surf", 16, True), ("surf", 64, True)],
+                         ids=["h2o2", "gri", "surf", "gas_surf", "h2o2-dq", "gri-dq", "gas_surf-dq", "surf-dq"])
 def test_integrate_parity(pkg, orc, gpu, case, N, dq):
     """Every reactor: same status (Success), the same ignition time to within the width of the
     ignition step (the marker's resolution), states at the 28 output times within the case's bounds
@@ -197,7 +197,7 @@ def test_integrate_parity(pkg, orc, gpu, case, N, dq):
     step count to 35 % per reactor and 3 % over the slice (rounding changes step sequences).
     Both engines use the analytic Jacobian by default; the "-dq" cases run CVODE's DQ Jacobian
     (br_opts.dq_jacobian, the reference's setting: the quad engine for H2/O2, the wavefront engine
-    for GRI and gas+surface) against the oracle's DQ run."""
+    for GRI, gas+surface and the 32-wide-vector surface-only case) against the oracle's DQ run."""
     from batchreactor_amd import ensemble
     pm, om = _mechs(pkg, orc, case)
     eng = pkg.Engine(pm)
