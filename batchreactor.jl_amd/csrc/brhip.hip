@@ -24,7 +24,6 @@
 #define BR_PHASE_CLOCKS 0   // per-phase shader-clock counters in br_stats (diagnostic build: libbrhip_diag.so)
 #endif
 #include "brhip_device.hpp"
-#include "brhip_lug.hpp"   // the lane-grid LU (BR_LU_GRID)
 // Diagnostic-only instruction-count experiments (scripts/micro/exp_hooks.hpp: a phase run twice,
 // extra VALU or memory work per Newton iteration) attach at these points of k_integrate; the
 // product build leaves them empty.
@@ -1071,9 +1070,12 @@ __device__ __forceinline__ void dq_column(LCtl* C, VA<CPL, GW, VS>& V, int lane,
     const double ij = (j < 64) ? gbcast<GW>(inc[0], j) : gbcast<GW>(inc[CPL - 1], j - 64);
     const double ii = 1.0 / ij;
     BR_GLOBAL double* col = launder(Jsave) + (size_t)j * JW;
+    const int n = gui<GW>(C->a_n);
+    // rows >= n stored as 0 (with 32-wide vectors lanes 32..63 read lane - 32's V_TEMP, and f is 0
+    // there: no consumer of Jsave has to mask them)
 #pragma unroll
     FOR_S {
-        const double v = ii * f[s] - ii * V.at(V_TEMP, s);
+        const double v = CS < n ? ii * f[s] - ii * V.at(V_TEMP, s) : 0.0;
         if (s == 0) col[lane] = v;
         else if (lane < 16) col[64 + lane] = v;
     }
@@ -1096,32 +1098,10 @@ __device__ __forceinline__ void dq_newton_rhs(LCtl* C, VA<CPL, GW, VS>& V, int l
 #ifndef BR_WPE
 #define BR_WPE 2
 #endif
-#ifndef BR_LU_MFMA
-// 32 < NMAX <= 64: 1 = blocked LU with fp64 MFMA trailing updates (lu_factor_mf) in the integrator;
-// 0 (default) = the row-per-lane VALU LU. Measured in-engine on GRI (round 4,
-// profiles/r04_lu_mfma_ab.json): MFMA 88.8k (panel 8) / 92.0k (panel 16) vs VALU 110.5k reactors/s --
-// the trailing matrix streams through the workspace (writes 6.6 -> 17 MB per reactor, wave time
-// parked in s_waitcnt 7.7 -> 13.6 M cycles) and costs more than the 12 % of VALU it saves.
-// lu_factor_mf stays built and tested (br_debug_lu_solve_mf).
-#define BR_LU_MFMA 0
-#endif
-// CPL = 1, NMAX 32 / 56 / 64: 1 = the 4 x 16 lane-grid LU (lu_factor_g, brhip_lug.hpp: pivot-row
-// values broadcast by the FMA's DPP modifier instead of a v_readlane pair per element, multipliers
-// exchanged through LDS; bit-identical factors, GPU suite and bitcmp); 0 (default) = the row-per-lane
-// lu_factor. Measured in-engine (round 5, profiles/r05_lu_ab.json): GRI
-// (NMAX 56) -3.1 %, so off there; the surface-only case (NMAX 32) +0.3 % in a same-session re-run
-// (BR_LU_GRID32 selects it for k_integrate<32> alone). Off by default: a semantically equivalent
-// refactor of its pivot handler gave wrong surface integrations in the engine while the micro harness
-// stayed bit-identical, so the code is not robust enough for a 0.3 % gain
-#ifndef BR_LU_GRID
-#define BR_LU_GRID 0
-#endif
-#ifndef BR_LU_GRID32
-#define BR_LU_GRID32 0
-#endif
-__host__ __device__ constexpr bool lu_grid(int nmax) {
-    return (BR_LU_GRID && (nmax == 32 || nmax == 56 || nmax == 64)) || (BR_LU_GRID32 && nmax == 32);
-}
+// (Measured and not adopted, round 4-5; DESIGN.md section 3: the blocked LU with fp64 MFMA trailing
+// updates -- GRI 88.8k / 92.0k vs 110.5k reactors/s, now in the variant library
+// csrc/variants/brhip_lumf.hip -- and the 4 x 16 lane-grid LU with DPP-broadcast FMAs -- GRI -3.1 %,
+// removed in round 6; it stays in the git history before that round.)
 // upper bound of reactors (waves) per workgroup for the occupancy search: gas+surface (n > 64)
 // needs 21 KB of LDS per reactor (+18 KB of tables), so only one workgroup of up to 6 reactors
 // (tables staged once) fits a CU's 160 KB: 6 waves/CU instead of 4 with 1-reactor workgroups;
@@ -1323,16 +1303,7 @@ __global__ __launch_bounds__(64 * br_maxrpb(NMAX)) __attribute__((amdgpu_waves_p
                 BR_ACC(cyc_jac, c0);
             }
             BR_CLK(c1);
-            if constexpr (CPL == 1 && NMAX > 32 && BR_LU_MFMA) {
-                // blocked LU, trailing updates on the fp64 matrix pipe; its E' staging uses the
-                // species block (idle between the Jacobian and the next RHS), whose conc[ONE] = 1.0
-                // pad slot (set once per reactor by init_tconst) is put back afterwards
-                lu_fail = lu_factor_mf<NMAX>(Jsave, LUsave, (LDSd*)S.sp, ud(C->gamma), n, lane, perm[0]);
-                wave_sync();
-                if (lane == 0) S.sp[Lay<CPL>::ONE] = 1.0;
-            } else if constexpr (CPL == 1 && lu_grid(NMAX)) {
-                lu_fail = lu_factor_g<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm[0]);
-            } else if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
+            if constexpr (CPL == 1) lu_fail = lu_factor<NMAX>(Jsave, LUsave, ud(C->gamma), n, lane, perm[0]);
             else lu_fail = lu_factor2<NMAX>(Jsave, LUsave, scr, ud(C->gamma), n, lane, perm);
             BR_ACC(cyc_lu, c1);
         }
@@ -2348,7 +2319,7 @@ int br_integrate_multi(br_mech* const* mechs, int ndev, int N, const double* T, 
 // solve one right-hand side per matrix. J[N][n][n] row-major, b/x [N][n].
 // ------------------------------------------------------------------------------------
 namespace {
-template <int NMAX, bool MF = (NMAX > 32 && BR_LU_MFMA)>
+template <int NMAX>
 __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, const double* g, const double* b,
                                                  double* x, double* ws, int* fail) {
     const int rid = blockIdx.x;
@@ -2364,11 +2335,7 @@ __global__ __launch_bounds__(64) void k_lu_check(int N, int n, const double* J, 
     // search + gather path), the second in the first one's pivot order (every pivot on its own lane:
     // the factors come out in step order, no gather); the solve uses the second one's factors
     int perm = lane;
-    auto factor = [&]() __attribute__((always_inline)) {
-        if constexpr (MF) return lu_factor_mf<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
-        else if constexpr (lu_grid(NMAX)) return lu_factor_g<NMAX>(Jt, LU, (LDSd*)prow, g[rid], n, lane, perm);
-        else return lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm);
-    };
+    auto factor = [&]() __attribute__((always_inline)) { return lu_factor<NMAX>(Jt, LU, g[rid], n, lane, perm); };
     int f = factor();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
@@ -2413,33 +2380,6 @@ __global__ __launch_bounds__(64) void k_lu_check2(int N, int n, const double* J,
 }
 }  // namespace
 
-// diagnostic (not in brhip.h): the factor workspace [M | D^-1] and the step -> row map after one
-// (twice = 0) or two factorizations of I - gamma J, for checking the LU against a lane-level
-// emulation (scripts/emu/lu_mf_emu.py). J[N][n][n] row-major; F[N][lu_ws_doubles(nmax)], perm[N][64].
-namespace {
-template <int NMAX, int STOP>
-__global__ __launch_bounds__(64) void k_lu_factor_dbg(int N, int n, const double* J, const double* g, int twice,
-                                                      double* ws, double* Fout, int* pout) {
-    const int rid = blockIdx.x;
-    if (rid >= N) return;
-    const int lane = threadIdx.x;
-    __shared__ double scr[256];
-    double* Jt = ws + (size_t)rid * (NMAX * WAVE + lu_ws_doubles(NMAX));
-    double* LU = Jt + NMAX * WAVE;
-    for (int j = 0; j < NMAX; ++j) Jt[j * WAVE + lane] = (lane < n && j < n) ? J[((size_t)rid * n + lane) * n + j] : 0.0;
-    for (int i = lane; i < lu_ws_doubles(NMAX); i += 64) LU[i] = __builtin_nan("");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    int perm = lane;
-    for (int r = 0; r <= twice; ++r) {
-        lu_factor_mf<NMAX, STOP>(Jt, LU, (LDSd*)scr, g[rid], n, lane, perm);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-    }
-    for (int i = lane; i < lu_ws_doubles(NMAX); i += 64) Fout[(size_t)rid * lu_ws_doubles(NMAX) + i] = LU[i];
-    pout[(size_t)rid * 64 + lane] = perm;
-}
-}  // namespace
 // device buffers of the diagnostic entry points below, freed on every exit path (HIPCHK returns early)
 namespace {
 struct DevScratch {
@@ -2456,33 +2396,6 @@ struct DevScratch {
     }
 };
 }  // namespace
-
-extern "C" int br_debug_lu_factor(int N, int n, const double* J, const double* gamma, int twice, int stop, double* F,
-                                  int* perm) {
-    if (N <= 0 || n <= 32 || n > 64) return fail_code_input();
-    const int nmax = n <= 56 ? 56 : 64;
-    const size_t lw = lu_ws_doubles(nmax);
-    double *dJ, *dg, *dws, *dF;
-    int* dp;
-    DevScratch S;
-    HIPCHK(S.alloc(&dJ, (size_t)N * n * n * 8));
-    HIPCHK(S.alloc(&dg, (size_t)N * 8));
-    HIPCHK(S.alloc(&dws, (size_t)N * (nmax * WAVE + lw) * 8));
-    HIPCHK(S.alloc(&dF, (size_t)N * lw * 8));
-    HIPCHK(S.alloc(&dp, (size_t)N * 64 * 4));
-    HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(N), dim3(64), 0, 0, N, n, dJ, dg, twice, dws, dF, dp); };
-    if (nmax == 56) {
-        if (stop == 0) go(k_lu_factor_dbg<56, 0>);
-        else if (stop == 1) go(k_lu_factor_dbg<56, 1>);
-        else go(k_lu_factor_dbg<56, (1 << 20)>);
-    } else go(k_lu_factor_dbg<64, (1 << 20)>);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(F, dF, (size_t)N * lw * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(perm, dp, (size_t)N * 64 * 4, hipMemcpyDeviceToHost));
-    return 0;
-}
 
 extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* gamma, const double* b, double* x,
                                  int* fail_out) {
@@ -2510,47 +2423,6 @@ extern "C" int br_debug_lu_solve(int N, int n, const double* J, const double* ga
     HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));
     return 0;
 }
-
-// diagnostic (not in brhip.h): br_debug_lu_solve with the MFMA-blocked LU (lu_factor_mf), 32 < n <= 64
-extern "C" int br_debug_lu_solve_mf(int N, int n, const double* J, const double* gamma, const double* b, double* x,
-                                    int* fail_out) {
-    if (N <= 0 || n <= 32 || n > 64) return fail_code_input();
-    const int nmax = n <= 56 ? 56 : 64;
-    double *dJ, *dg, *db, *dx, *dws;
-    int* df;
-    DevScratch S;
-    HIPCHK(S.alloc(&dJ, (size_t)N * n * n * 8));
-    HIPCHK(S.alloc(&dg, (size_t)N * 8));
-    HIPCHK(S.alloc(&db, (size_t)N * n * 8));
-    HIPCHK(S.alloc(&dx, (size_t)N * n * 8));
-    HIPCHK(S.alloc(&dws, (size_t)N * (nmax * col_rows(nmax) + lu_ws_doubles(nmax)) * 8));
-    HIPCHK(S.alloc(&df, (size_t)N * 4));
-    HIPCHK(hipMemcpy(dJ, J, (size_t)N * n * n * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(dg, gamma, (size_t)N * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(db, b, (size_t)N * n * 8, hipMemcpyHostToDevice));
-    if (nmax == 56) hipLaunchKernelGGL((k_lu_check<56, true>), dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
-    else hipLaunchKernelGGL((k_lu_check<64, true>), dim3(N), dim3(64), 0, 0, N, n, dJ, dg, db, dx, dws, df);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(x, dx, (size_t)N * n * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(fail_out, df, (size_t)N * 4, hipMemcpyDeviceToHost));
-    return 0;
-}
-
-#if BR_LUG_STATS
-// diagnostic build only (not declared in brhip.h): read and reset the grid-LU event counts
-// (brhip_lug.hpp: factorizations, steps, pivot handler calls, ties, interchanges, sum of their steps)
-extern "C" int br_debug_lug_stats(double* out8) {
-    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(brhip::g_lug_stats), sizeof v) != hipSuccess) return -1;
-    for (int i = 0; i < 8; ++i) out8[i] = (double)v[i];
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(brhip::g_lug_stats), z, sizeof z) != hipSuccess) return -1;
-    return 0;
-}
-extern "C" int br_debug_lug_dump(unsigned long long* out2048) {
-    return hipMemcpyFromSymbol(out2048, HIP_SYMBOL(brhip::g_lug_dump), 256 * 8 * 8) == hipSuccess ? 0 : -1;
-}
-#endif
 
 #if BR_PHASE_CLOCKS
 // diagnostic build only (not declared in brhip.h): read and reset the 16 sub-phase clock sums

@@ -1312,283 +1312,8 @@ __device__ __forceinline__ int lu_factor(const double* __restrict__ J_, double* 
     return fail;
 }
 
-// ------------------------------------------------------------------------------------
-// Blocked LU for 32 < NMAX <= 64 (CPL = 1) with the trailing update on the fp64 matrix pipe
-// (v_mfma_f64_16x16x4f64). Same pivoting rule, multipliers and stored factor form as lu_factor
-// (SUNDIALS denseGETRF semantics; rows loaded in the previous pivot order; factors in M, step
-// order after the gather); the trailing update is reassociated (bands, not bits, against the
-// unblocked form).
-//
-// Panels of 16 columns, factored right-looking row-per-lane (pivot search and readlane
-// broadcasts as lu_rl_steps). Alongside, each panel tracks E' (64 x 16, row per lane):
-// E = the same elimination applied to [0; I] on the panel's pivot rows (E[p_j] = (L11^-1)_j,
-// E[r] = -(L21 L11^-1)_r for rows not yet pivoted, 0 for rows pivoted earlier), E' = E - the
-// pivot entries (E'[p_j][j] = 0). Then the whole right-looking update of the trailing columns by
-// the panel's 16 steps is one GEMM over ALL rows, no mask:
-//     X <- X + E' X[piv]   (pivot rows get L11^-1 X[piv] = U12, the other rows X - L21 U12).
-// It runs transposed, X^T (cols x rows) += X[piv]^T (cols x 16) E'^T (16 x rows), so that the
-// accumulator layout (col = 16c + (lane >> 4) + 4 i, row = 16t + (lane & 15)) addresses the
-// column-major factor matrix M in 128-B row segments, and the trailing matrix lives in M itself:
-// column j of X sits where factor column j will be written, and panel p reads its columns from
-// there before its steps overwrite them with factors. Operands: A = X[piv]^T gathered from M
-// (lane: col 16c + (lane & 15), k = 4s + (lane >> 4)); B = E'^T through LDS scratch (one 4-column
-// chunk of E' at a time, 2 KB). Row tiles whose rows were all pivoted before the panel have E' = 0
-// and are skipped (with the rows in the previous pivot order that is every earlier tile).
-// ------------------------------------------------------------------------------------
-typedef double d4v __attribute__((ext_vector_type(4)));
-
-#ifndef BR_LU_PW
-#define BR_LU_PW 8   // panel width of lu_factor_mf (8 or 16)
-#endif
-
-// one panel: columns c0 .. c0+PW-1 right-looking in a[] (row per lane), factor columns stored to
-// M as each step completes, E' in e[] (WITH_E), the steps' pivot lanes in piv[]
-template <int FR, int PW, bool WITH_E>
-__device__ __forceinline__ void lu_mf_panel(double (&a)[PW], double (&e)[PW], int (&piv)[PW], int c0, int nlive,
-                                            int lane, int prow, int& pstep, double& dinv, int& fail,
-                                            __amdgpu_buffer_rsrc_t rs) {
-    const unsigned fo8 = (lane < FR) ? (unsigned)lane * 8u : LU_OOB;
-#pragma unroll
-    for (int kk = 0; kk < PW; ++kk) {
-        if (kk < nlive) {
-            const int k = c0 + kk;
-            const bool cand = pstep < 0;
-            const int p = pivot_lane(a[kk], cand ? 0x7fffffffu : 0u, prow);
-            piv[kk] = p;
-            const double pv = bcast(a[kk], p);
-            if (pv == 0.0 && !fail) fail = k + 1;
-            const double rinv = 1.0 / pv;
-            const bool isp = (lane == p);
-            const bool rem = cand && !isp;
-            const double l = rem ? a[kk] * rinv : 0.0;
-            const double fv = rem ? l : (cand ? 0.0 : a[kk] * dinv);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fv), rs, fo8, k * (FR * 8), 0);
-            if (isp) { pstep = k; dinv = rinv; }
-            if constexpr (WITH_E) {
-#pragma unroll
-                for (int j = 0; j < kk; ++j) e[j] = fma(-bcast_lu(e[j], p), l, e[j]);
-                e[kk] = -l;
-            }
-            int nl = nlive;   // (opaque per step: scalar tests, see lu_factor)
-            asm volatile("" : "+s"(nl));
-#pragma unroll
-            for (int j = kk + 1; j < PW; ++j)
-                if (j < nl) a[j] = fma(-bcast_lu(a[j], p), l, a[j]);
-        }
-    }
-}
-
-template <int NMAX, int STOP = (1 << 20)>   // STOP: return after that panel's trailing update (debug kernel)
-__device__ __forceinline__ int lu_factor_mf(const double* __restrict__ J_, double* __restrict__ ws, LDSd* scr,
-                                            double gamma, int n, int lane, int& perm_io) {
-    static_assert(NMAX > 32 && NMAX <= 64 && NMAX % 8 == 0, "lu_factor_mf: NMAX");
-    constexpr int PW = BR_LU_PW;             // panel width
-    constexpr int KS = PW / 4;               // MFMA k-steps per panel
-    constexpr int FR = NMAX;                 // factor column stride (rows)
-    constexpr int NRT = (NMAX + 15) / 16;    // row tiles
-    constexpr int MAXCT = (NMAX - PW + 15) / 16;   // column tiles of the largest trailing block
-    static_assert(PW == 8 || PW == 16, "lu_factor_mf: PW");
-    const BR_GLOBAL double* J = launder(J_);
-    BR_GLOBAL double* wsg = launder(ws);
-    const LUWs F{wsg, wsg + NMAX * FR};
-    const __amdgpu_buffer_rsrc_t rs = lu_rsrc(wsg, NMAX * FR);
-    lane = launder_v(lane);
-    n = launder_s(n);
-    // the trailing block's pivot-row operand through a buffer of n columns: padding columns read 0
-    const __amdgpu_buffer_rsrc_t rsn = lu_rsrc(wsg, n * FR);
-    const __amdgpu_buffer_rsrc_t rj = __builtin_amdgcn_make_buffer_rsrc((void*)J, (short)0, n * (WAVE * 8), 0x00020000);
-    const int prow = launder_v(perm_io);
-    const bool act = lane < n;
-    const int g = lane >> 4, m = lane & 15;
-    int pstep = act ? -1 : 1024;
-    double dinv = 0.0;
-    int fail = 0;
-    const int np = (n + PW - 1) / PW;
-    const unsigned fo8 = (lane < FR) ? (unsigned)lane * 8u : LU_OOB;
-#pragma unroll 1
-    for (int p = 0; p + 1 < np; ++p) {
-        BR_SUB_T(lt0);
-        const int c0 = PW * p;
-        const unsigned long long live = __ballot(pstep < 0);   // rows not pivoted before this panel
-        double a[PW], e[PW];
-        int piv[PW];
-#pragma unroll
-        for (int j = 0; j < PW; ++j) e[j] = 0.0;
-        if (p == 0) {
-            const unsigned jo8 = act ? (unsigned)prow * 8u : LU_OOB;
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                const double jv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rj, jo8 + j * (WAVE * 8), 0, 0));
-                a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < PW; ++j)
-                a[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, fo8 + j * (FR * 8), c0 * (FR * 8), 0));
-        }
-        lu_mf_panel<FR, PW, true>(a, e, piv, c0, PW, lane, prow, pstep, dinv, fail, rs);
-        // ---- E'^T operands through LDS, one 4-column chunk at a time: lane l of operand (t, s)
-        // holds E'[16t + (l & 15)][4s + (l >> 4)]
-        double bo[NRT][KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) scr[4 * lane + q] = e[4 * s + q];
-            wave_sync();
-#pragma unroll
-            for (int t = 0; t < NRT; ++t) bo[t][s] = scr[4 * (16 * t + m) + g];
-            wave_sync();
-        }
-        // A operand rows: the pivot row of step 4s + (lane >> 4); in the first panel the trailing
-        // columns are still I - gamma J, read from J at the pivot's original row (aor)
-        unsigned ao8[KS];
-        int aor[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int pr = g == 0 ? piv[4 * s] : g == 1 ? piv[4 * s + 1] : g == 2 ? piv[4 * s + 2] : piv[4 * s + 3];
-            if (p == 0) {
-                aor[s] = __builtin_amdgcn_ds_bpermute(4 * pr, prow);
-                ao8[s] = (unsigned)aor[s] * 8u + (unsigned)m * (WAVE * 8);
-            } else {
-                ao8[s] = (unsigned)(m * FR + pr) * 8u;
-            }
-        }
-        // first trailing update: X = I - gamma J straight from the saved J; position 16t + m holds
-        // original row orow[t] (-1: none; its J offset out of range)
-        unsigned jt8[NRT];
-        int orow[NRT];
-        if (p == 0) {
-#pragma unroll
-            for (int t = 0; t < NRT; ++t) {
-                orow[t] = __builtin_amdgcn_ds_bpermute(4 * (16 * t + m), act ? prow : -1);
-                jt8[t] = orow[t] >= 0 ? (unsigned)orow[t] * 8u + (unsigned)g * (WAVE * 8) : LU_OOB;
-            }
-        }
-        // accumulator rows 16t + m (out of range for rows >= FR)
-        unsigned rb8[NRT];
-#pragma unroll
-        for (int t = 0; t < NRT; ++t) rb8[t] = (16 * t + m < FR) ? (unsigned)(g * FR + 16 * t + m) * 8u : LU_OOB;
-        BR_SUB_ADD(0, lt0);
-        BR_SUB_T(lt1);
-        // ---- trailing update: columns c0 + PW .. n-1 in tiles of 16
-        const int cs = c0 + PW;
-#pragma unroll
-        for (int ct = 0; ct < MAXCT; ++ct) {
-            const int cb = cs + 16 * ct;
-            if (cb < n) {
-                double ao[KS];
-#pragma unroll
-                for (int s = 0; s < KS; ++s) {
-                    if (p == 0) {
-                        const double jv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rj, ao8[s] + cb * (WAVE * 8), 0, 0));
-                        ao[s] = ((aor[s] == cb + m) ? 1.0 : 0.0) - gamma * jv;
-                    } else {
-                        ao[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsn, ao8[s] + cb * (FR * 8), 0, 0));
-                    }
-                }
-                d4v x[NRT];
-#pragma unroll
-                for (int t = 0; t < NRT; ++t) {
-                    if ((live >> (16 * t)) & 0xffffull) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int cc = cb + 4 * i;   // columns cc .. cc + 3 (lane groups)
-                            x[t][i] = 0.0;
-                            if (cc < NMAX) {
-                                if (p == 0) {
-                                    const double jv = __builtin_bit_cast(double,
-                                        __builtin_amdgcn_raw_buffer_load_b64(rj, jt8[t] + cc * (WAVE * 8), 0, 0));
-                                    x[t][i] = ((orow[t] == cc + g) ? 1.0 : 0.0) - gamma * jv;
-                                } else {
-                                    x[t][i] = __builtin_bit_cast(double,
-                                        __builtin_amdgcn_raw_buffer_load_b64(rs, rb8[t], cc * (FR * 8), 0));
-                                }
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < NRT; ++t) {
-                    if ((live >> (16 * t)) & 0xffffull) {
-#pragma unroll
-                        for (int s = 0; s < KS; ++s) x[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ao[s], bo[t][s], x[t], 0, 0, 0);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int cc = cb + 4 * i;
-                            // (through a scalar copy: __builtin_bit_cast of a vector element reads element 0)
-                            const double xv = x[t][i];
-                            if (cc < NMAX)
-                                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, xv), rs, rb8[t], cc * (FR * 8), 0);
-                        }
-                    }
-                }
-            }
-        }
-        BR_SUB_ADD(1, lt1);
-        if (p == STOP) {
-            perm_io = prow;
-            return 0;
-        }
-    }
-    {   // last panel: no trailing columns, no E'
-        BR_SUB_T(lt0);
-        const int c0 = PW * (np - 1);
-        double a[PW], e[PW];
-        int piv[PW];
-        const int nlive = n - c0;
-        if (np == 1) {
-            const unsigned jo8 = act ? (unsigned)prow * 8u : LU_OOB;
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                const double jv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rj, jo8 + j * (WAVE * 8), 0, 0));
-                a[j] = ((j == prow) ? 1.0 : 0.0) - gamma * jv;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                a[j] = 0.0;
-                if (j < nlive)
-                    a[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, fo8 + j * (FR * 8), c0 * (FR * 8), 0));
-            }
-        }
-        lu_mf_panel<FR, PW, false>(a, e, piv, c0, nlive, lane, prow, pstep, dinv, fail, rs);
-        BR_SUB_ADD(0, lt0);
-    }
-    BR_SUB_T(lt2);
-    constexpr int CH = 8, NC = NMAX / CH;
-    int perm;
-    if (__ballot(act && pstep != lane) == 0) {
-        // pivots in lane order: M is in step order already; padding columns n..NMAX-1 zeroed
-        perm = prow;
-        if (lane < FR)
-            for (int c = n; c < NMAX; ++c) F.M[c * FR + lane] = 0.0;
-        F.D[lane] = dinv;
-    } else {
-        // rows into step order, in place (as lu_factor; columns >= n: zeros)
-        const int q = pivot_perm(pstep, lane, n);
-        perm = __builtin_amdgcn_ds_bpermute(q * 4, prow);
-        double gb[2][CH];
-        auto gather = [&](double (&v)[CH], int c) {
-#pragma unroll
-            for (int i = 0; i < CH; ++i) v[i] = F.M[min(c + i, n - 1) * FR + min(q, FR - 1)];
-        };
-        gather(gb[0], 0);
-#pragma unroll
-        for (int t = 0; t < NC; ++t) {
-            if (t + 1 < NC) gather(gb[(t + 1) & 1], (t + 1) * CH);
-            __builtin_amdgcn_sched_barrier(0);
-            if (lane < FR) {
-#pragma unroll
-                for (int i = 0; i < CH; ++i) F.M[(t * CH + i) * FR + lane] = (t * CH + i < n) ? gb[t & 1][i] : 0.0;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        F.D[lane] = lane_pull(dinv, q);
-    }
-    BR_SUB_ADD(2, lt2);
-    perm_io = perm;
-    return fail;
-}
+// (The blocked LU with fp64 MFMA trailing updates, lu_factor_mf, measured and not adopted in round 4,
+// lives in the variant library csrc/variants/brhip_lumf.hip -> libbrhip_lumf.so since round 6.)
 
 // ---- triangular sweeps in DPP form: the columns go in blocks of 16, one block per 16-lane DPP
 // row. Block b first runs its diagonal 16 x 16 part inside row b: r += -M[s][k] * r[k], with r[k]
@@ -1606,11 +1331,17 @@ __device__ __forceinline__ void dpp_fnma_self(double& r, double f) {
     asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, -%1 row_newbcast:%2 row_mask:%3 bank_mask:0xf"
                  : "+v"(r) : "v"(f), "i"(K), "i"(RM));
 }
-// r += -f * x[row base + K] in the rows of RM
-template <int K, int RM>
+// r += -f * x[row base + K] in the rows of RM. x is the DPP-read operand: the first op of a chain
+// (NOP) carries the s_nop itself, since LLVM's hazard recognizer does not see a DPP read inside
+// inline asm and may place a VALU copy of x right before it; later ops of the chain read the same x
+template <int K, int RM, bool NOP = false>
 __device__ __forceinline__ void dpp_fnma(double& r, double x, double f) {
-    asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:%4 bank_mask:0xf"
-                 : "+v"(r) : "v"(x), "v"(f), "i"(K), "i"(RM));
+    if constexpr (NOP)
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:%4 bank_mask:0xf"
+                     : "+v"(r) : "v"(x), "v"(f), "i"(K), "i"(RM));
+    else
+        asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:%4 bank_mask:0xf"
+                     : "+v"(r) : "v"(x), "v"(f), "i"(K), "i"(RM));
 }
 template <bool FWD, int CW, int RM, int I>
 __device__ __forceinline__ void dpp_diag(double& r, const double (&v)[16]) {
@@ -1624,7 +1355,7 @@ template <bool FWD, int CW, int RM, int I>
 __device__ __forceinline__ void dpp_off(double& r, double x, const double (&v)[16]) {
     if constexpr (I < CW) {
         constexpr int K = FWD ? I : CW - 1 - I;
-        dpp_fnma<K, RM>(r, x, v[K]);
+        dpp_fnma<K, RM, I == 0>(r, x, v[K]);
         dpp_off<FWD, CW, RM, I + 1>(r, x, v);
     }
 }

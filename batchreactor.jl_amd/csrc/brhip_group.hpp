@@ -17,18 +17,11 @@
 // reaction | fod: {k0/kinf, log10 Fcent, c, n} per falloff reaction | skd: k(T) per surface
 // reaction]. Global: the saved Jacobian, GL x GL column-major per group slot. Mechanism tables as for
 // the wavefront engine (LDS image, records with the pad species 64 = conc 1.0).
-// BR_QKD_GLOBAL=1: kd lives in the group's global slot after its saved Jacobian (L2-resident: a
-// few hundred bytes per group), and a gas-only 16-lane species block drops its surface sums (66
-// doubles instead of 82): 2.38 instead of 2.83 KB of LDS per H2/O2 reactor, so four 16-reactor
-// workgroups (16 waves) fit a CU's 160 KB instead of three.
+// kd lives in the group's global slot after its saved Jacobian (L2-resident: a few hundred bytes per
+// group), and a gas-only 16-lane species block drops its surface sums (66 doubles instead of 82):
+// 2.38 instead of 2.83 KB of LDS per H2/O2 reactor, so four 16-reactor workgroups (16 waves) fit a
+// CU's 160 KB instead of three (round 5: C2 +11 %; kd in LDS was the round-4 layout).
 #pragma once
-
-#ifndef BR_QKD_GLOBAL
-#define BR_QKD_GLOBAL 1
-#endif
-#ifndef BR_QVS
-#define BR_QVS 0
-#endif
 
 namespace grp {
 // species block of a group (doubles): conc[CONC + k], gas production sums ACCW, surface production
@@ -43,34 +36,25 @@ struct GLay {
     static_assert(ONE == Lay<1>::ONE, "pad species");
 };
 constexpr int MAX_SETS = 32;
-// BR_QVS = 1: Nordsieck / work vectors NM wide (the register width >= n: 9 for H2/O2) instead of GL;
-// lanes nm..GL-1 of a group read the last entry and never store (VProxy), 560 B less LDS per H2/O2
-// reactor, enough for five workgroups per CU. Measured (round 5, profiles/r05_h2o2_quad_wpe_ab.json):
-// 1.078M at 4 waves/SIMD and 798k at 5 (96 VGPRs, 284 B/lane spilled) vs 1.096M -- off
-__host__ __device__ constexpr int vstride(int gl, int nm) { return BR_QVS ? nm : gl; }
+// (Nordsieck / work vectors NM wide instead of GL measured 1.078M vs 1.096M reactors/s, round 5,
+// profiles/r05_h2o2_quad_wpe_ab.json; not kept)
+__host__ __device__ constexpr int vstride(int gl, int nm) { return nm > 0 ? gl : gl; }
 __host__ __device__ inline int vbytes(int gl, int nm) { return NVEC * vstride(gl, nm) * 8; }
 __host__ __device__ inline int sp_off(int gl, int nm) { return CTL_BYTES + vbytes(gl, nm); }
 // species-block doubles: gas-only 16-lane groups need no surface sums (ACCS) past ONE = 64
 __host__ __device__ inline int sp_doubles(int gl, int nrs) {
-    return gl == 16 ? ((BR_QKD_GLOBAL && nrs == 0) ? 66 : GLay<16>::DOUBLES) : GLay<32>::DOUBLES;
+    return gl == 16 ? (nrs == 0 ? 66 : GLay<16>::DOUBLES) : GLay<32>::DOUBLES;
 }
-// kd in LDS (BR_QKD_GLOBAL 0): right after the species block
-__host__ __device__ inline int kd_off(int gl, int nm, int nrs) { return sp_off(gl, nm) + sp_doubles(gl, nrs) * 8; }
-__host__ __device__ inline int kd_lds_bytes(int nrg) { return BR_QKD_GLOBAL ? 0 : 16 * nrg; }
-__host__ __device__ inline int fod_off(int gl, int nm, int nrg, int nrs) { return kd_off(gl, nm, nrs) + kd_lds_bytes(nrg); }
+__host__ __device__ inline int fod_off(int gl, int nm, int nrg, int nrs) { (void)nrg; return sp_off(gl, nm) + sp_doubles(gl, nrs) * 8; }
 __host__ __device__ inline int block_bytes(int gl, int nm, int nrg, int nfo, int nrs) {
     const int b = fod_off(gl, nm, nrg, nrs) + 32 * nfo + 8 * nrs;
     return (b + 15) / 16 * 16;
 }
-// global doubles per group slot: the saved Jacobian (GL x GL), then kd when BR_QKD_GLOBAL (64-B aligned)
-// (at least 8: the RHS prefetches the pair of reaction 0 even when there are no gas reactions)
-__host__ __device__ inline int slot_doubles(int gl, int nrg) { return gl * gl + (BR_QKD_GLOBAL ? ((2 * nrg + 7) / 8 * 8 > 8 ? (2 * nrg + 7) / 8 * 8 : 8) : 0); }
+// global doubles per group slot: the saved Jacobian (GL x GL), then kd (64-B aligned; at least 8: the
+// RHS prefetches the pair of reaction 0 even when there are no gas reactions)
+__host__ __device__ inline int slot_doubles(int gl, int nrg) { return gl * gl + ((2 * nrg + 7) / 8 * 8 > 8 ? (2 * nrg + 7) / 8 * 8 : 8); }
 }  // namespace grp
-#if BR_QKD_GLOBAL
 typedef BR_GLOBAL double QKd;   // {kf, kr} pairs: the group slot in global memory
-#else
-typedef double QKd;
-#endif
 
 // max of a 32-bit value over each 16-lane DPP row (every lane gets its row's max)
 __device__ __forceinline__ unsigned row_umax(unsigned x) {
@@ -186,12 +170,10 @@ __device__ __forceinline__ void g_init_tconst(const Tab& tb, double* sp, QKd* kd
         else k = spr[0] * pow(T, spr[1]) * exp(-spr[2] / RT);
         skd[r] = k;
     }
-#if BR_QKD_GLOBAL
     // the kd stores reach L2 and this CU's L1 is invalidated before any lane reads the slot (it held
     // the previous reactor's constants), as init_tconst's RXD
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     wave_sync();
 }
 
@@ -232,7 +214,7 @@ __device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const QKd* kd
     const int n = MF(n), ng = MF(ng), nrg = MF(nrg), nrs = MF(nrs), nset = MF(nset);
     const bool gas = gl < ng;
     // the {kf, kr} pairs of this lane's first two gas reactions, issued before the concentration and
-    // third-body setup so their latency overlaps it (kd is in global memory with BR_QKD_GLOBAL)
+    // third-body setup so their latency overlaps it (kd is in global memory)
     const double2 kz = make_double2(0.0, 0.0);
     const double2 kp0 = nrg > 0 ? g_kpair(kd, gl < nrg ? gl : 0) : kz;
     const double2 kp1 = nrg > GL ? g_kpair(kd, gl + GL < nrg ? gl + GL : 0) : kz;
@@ -324,81 +306,9 @@ __device__ __forceinline__ double g_rhs(const Tab& tb, double* sp, const QKd* kd
     return 0.0;
 }
 
-// Analytic Jacobian d(du)/du of a gas-only group's reactor, row gl per lane (jr[j] = J[gl][j]), at
-// the state of the RHS just evaluated (its concentrations and third-body sums are still in the
-// species block). The same terms as the wavefront engine's jacobian() and the oracle's jac_tc:
-// J[k][j] = M_k / M_j sum_r nu_kr dq_r/dc_j (mass-action partial products, third-body / falloff d[M]
-// columns; the M_k / M_j factor applied once per entry). Reactions in a uniform loop (every group
-// evaluates reaction r for its own state); the sparse partials reach their column through scalar
-// compares on the uniform species.
-template <int GL, int NM>
-__device__ __forceinline__ void g_jac(const Tab& tb, const double* sp, const QKd* kd, const double* fod, int gl,
-                                      double (&jr)[NM]) {
-    typedef grp::GLay<GL> L;
-    const int n = MF(n), ng = MF(ng), nrg = MF(nrg);
-    const bool xm = (MF(conv) & 2) != 0;
-#pragma unroll
-    for (int j = 0; j < NM; ++j) jr[j] = 0.0;
-    const unsigned gl8 = (unsigned)gl * 8u;
-    // this row's net stoichiometric coefficient from a reaction's scatter list
-    auto row_nu = [&](uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
-        const int cnt = (int)(s3 >> 24);
-        const uint32_t sw[3] = {s0, s1, s2};
-        double nu = 0.0;
-#pragma unroll
-        for (int e = 0; e < 6; ++e)
-            if (e < cnt && sl_off(sw[e >> 1], e & 1) == gl8) nu += (double)sl_nu(s3, e);
-        return nu;
-    };
-#pragma unroll 1
-    for (int r = 0; r < nrg; ++r) {
-        const auto rr = rx_rec(tb.rx, r);
-        const uint32_t w0 = uni((int)rr[0]), w1 = uni((int)rr[1]), info = uni((int)rr[2]);
-        const uint32_t s0 = uni((int)rr[4]), s1 = uni((int)rr[5]), s2 = uni((int)rr[6]), s3 = uni((int)rr[7]);
-        double cf[4], cb[4];
-        const double D = g_mass_action<GL>(sp, kd, w0, w1, r, cf, cb);
-        double pre = 1.0, coefM = 0.0;
-        const int tbk = gi_tb(info);
-        if (tbk) {
-            const double Mc = sp[L::MC + gi_tbidx(info)];
-            if (tbk == 1) { pre = Mc; coefM = 1.0; }
-            else {
-                double fac, dfac;
-                falloff<true>(fod + 4 * gi_foidx(info), gi_troe(info) != 0, Mc, fac, dfac);
-                const double xs = xm ? Mc * 1e-6 : 1.0;               // [M] in mol/cm3 (reference)
-                pre = fac * xs;
-                coefM = dfac * xs + (xm ? fac * 1e-6 : 0.0);
-            }
-        }
-        const double nu = row_nu(s0, s1, s2, s3);
-        if (tbk) {                                                     // d q / d c_j = D coefM eff_j
-            const double dm = nu * D * coefM;
-            const double* eff = MF(tb_eff) + (size_t)gi_tbidx(info) * MF(n);
-#pragma unroll
-            for (int j = 0; j < NM; ++j) if (j < ng) jr[j] = fma(dm, eff[j], jr[j]);
-        }
-        const double kf = kd[2 * r], kr = kd[2 * r + 1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {                                  // slot e of the forward (backward) product
-            double pf = kf * pre, pb = -kr * pre;
-#pragma unroll
-            for (int e2 = 0; e2 < 4; ++e2)
-                if (e2 != e) { pf *= cf[e2]; pb *= cb[e2]; }
-            const int kfs = (int)((w0 >> (8 * e)) & 255), kbs = (int)((w1 >> (8 * e)) & 255);
-            const double vf = nu * pf, vb = nu * pb;
-#pragma unroll
-            for (int j = 0; j < NM; ++j) {
-                if (j == kfs) jr[j] += vf;   // (kfs, kbs uniform: scalar branches; pad slot 64 matches no j)
-                if (j == kbs) jr[j] += vb;
-            }
-        }
-    }
-    const double Mk = tb.molwt[gl];
-#pragma unroll
-    for (int j = 0; j < NM; ++j) jr[j] = (gl < ng && j < ng) ? jr[j] * (Mk / tb.molwt[j]) : 0.0;
-#pragma unroll
-    for (int j = 0; j < NM; ++j) if (!(gl < n && j < n)) jr[j] = 0.0;
-}
+// (A register-row gas Jacobian -- every group evaluates every reaction, the sparse partials reach
+// their column by scalar compares -- measured 902.2k vs 980.6k reactors/s for the column passes below,
+// 78.8k vs 40.3k cycles per Jacobian: round 4. Removed in round 6.)
 
 // Analytic Jacobian of a group's reactor with surface chemistry, in column passes as the wavefront
 // engine's general jacobian() (brhip_device.hpp; oracle jac_tc): for each component j, the reactions
@@ -611,22 +521,13 @@ __device__ __forceinline__ double g_solve(const double (&a)[NM], int orig, doubl
     return gl < n ? x : 0.0;
 }
 
-// the controller entry points for GL-lane groups (BR_QCTL_NOINLINE: out of line, so their register
-// allocation is separate from the hot loop's; measured: more VGPRs, kept inline)
-#ifndef BR_QCTL_NOINLINE
-#define BR_QCTL_NOINLINE 0
-#endif
-#if BR_QCTL_NOINLINE
-#define BR_QCTL_ATTR __noinline__
-#else
-#define BR_QCTL_ATTR __forceinline__
-#endif
+// the controller entry points for GL-lane groups (inline: out of line measured more VGPRs)
 template <int GL, int VS>
-__device__ BR_QCTL_ATTR int g_post_rhs(LCtl* C, VA<1, GL, VS>& V, int gl, const double (&f)[1], double (&b)[1]) {
+__device__ __forceinline__ int g_post_rhs(LCtl* C, VA<1, GL, VS>& V, int gl, const double (&f)[1], double (&b)[1]) {
     return ctl_post_rhs<1, GL>(C, V, gl, f, b);
 }
 template <int GL, int VS>
-__device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VA<1, GL, VS>& V, int gl, double (&delta)[1], int lu_fail) {
+__device__ __forceinline__ int g_post_solve(LCtl* C, VA<1, GL, VS>& V, int gl, double (&delta)[1], int lu_fail) {
     return ctl_post_solve<1, GL>(C, V, gl, delta, lu_fail);
 }
 
@@ -635,18 +536,12 @@ __device__ BR_QCTL_ATTR int g_post_solve(LCtl* C, VA<1, GL, VS>& V, int gl, doub
 // groups idle meanwhile): C2 993.8k vs 986.7k reactors/s at 2 (mean of two alternations, round 4)
 #define BR_GPRIO 2
 #endif
-#ifndef BR_QJAC_COLS
-// 1 (default): the column-pass Jacobian for gas-only mechanisms too; 0: register rows (g_jac). C2
-// H2/O2: 980.6k vs 902.2k reactors/s, 40.3k vs 78.8k cycles per Jacobian -- g_jac's per-entry scalar
-// compare-and-branch chains, and every cycle of a group's setup idles the other three groups (round 4)
-#define BR_QJAC_COLS 1
-#endif
 #ifndef BR_QWPB
 #define BR_QWPB 4   // waves per workgroup (16 quad / 8 pair reactors); tables staged once per workgroup
 #endif
 #ifndef BR_QWPE
 #define BR_QWPE 4   // waves per SIMD the register allocation targets for 16-lane groups (<= 128 VGPRs,
-                    // ~128 B/lane spilled). Quad H2/O2: with the LDS block cut to 2.38 KB (BR_QKD_GLOBAL),
+                    // ~128 B/lane spilled). Quad H2/O2: with the LDS block cut to 2.38 KB (kd global),
                     // four workgroups fit a CU: 1.100M reactors/s at 4 vs 981k at 3 (round 5); with the
                     // 2.83 KB block LDS capped it at 12 waves/CU (882k at 3 vs 693k at 2, round 4)
 #endif
@@ -676,11 +571,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
     double* fod = reinterpret_cast<double*>(rbase + grp::fod_off(GL, NM, MF(nrg), MF(nrs)));
     double* skd = fod + 4 * MF(nfo);
     const int SD = grp::slot_doubles(GL, MF(nrg));                      // global doubles per group slot
-#if BR_QKD_GLOBAL
     QKd* kd = launder(Jws) + (size_t)slot * SD + GL * GL;
-#else
-    QKd* kd = reinterpret_cast<double*>(rbase + grp::kd_off(GL, NM, MF(nrs)));
-#endif
     // the group's saved-J slot through a buffer resource: lane offset in a VGPR, the column offset
     // j GL 8 as the instruction's scalar offset (as 64-bit addresses, the columns past 4 KB of a 32-lane
     // slot were materialised per column, hoisted out of the loop and spilled)
@@ -821,16 +712,9 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
 #endif
                 if (!jac_ready && C->newj) {                            // analytic Jacobian at y, saved
                     QCLK(c_j);
-                    if (MF(nrs) == 0 && !BR_QJAC_COLS) {                // gas only: register rows
-                        double jr[NM];
-                        g_jac<GL, NM>(tb, sp, kd, fod, gl, jr);
-#pragma unroll
-                        for (int j = 0; j < NM; ++j) jst(j, jr[j]);
-                    } else {                                            // surface chemistry: column passes
-                        g_jac_cols<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, gl, jst);
+                    g_jac_cols<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, gl, jst);   // column passes
 #pragma unroll 1
-                        for (int j = n; j < NM; ++j) jst(j, 0.0);             // padding columns
-                    }
+                    for (int j = n; j < NM; ++j) jst(j, 0.0);                 // padding columns
                     QACC(q_jac_c, c_j);
                 }
                 QCLK(c_l);

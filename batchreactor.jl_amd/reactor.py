@@ -58,6 +58,21 @@ class ODEProblem:
     p: dict = field(default_factory=dict)
 
 
+# SciML return codes of a CVODE_BDF solve (Symbol(sol.retcode), src/BatchReactor.jl:216), from the
+# engine's per-reactor status (include/brhip.h): Sundials.jl's interpret_sundials_retcode maps CVODE's
+# flags -1 (CV_TOO_MUCH_WORK) -> MaxIters, -2 / -3 (CV_TOO_MUCH_ACC, CV_ERR_FAILURE) -> Unstable,
+# -4 (CV_CONV_FAILURE) -> ConvergenceFailure, any other failure -> Failure; SciML's unstable_check (a
+# NaN state) ends the solve with Unstable (status -7). Restated from the published packages, which are
+# not in the image: the mapping itself is parity-unpinned (no reference fixture fails).
+RETCODES = {0: "Success", -1: "MaxIters", -2: "Unstable", -3: "Unstable", -4: "ConvergenceFailure",
+            -7: "Unstable"}
+
+
+def retcode(status) -> str:
+    """The retcode symbol's name for an engine status code (0 -> "Success")."""
+    return RETCODES.get(int(status), "Failure")
+
+
 def _engine(mech: Mechanism, device=0) -> Engine:
     """One engine per (mechanism object, device), owned by the mechanism: it lives as long as the
     mechanism does (no global cache, so repeated file-driven calls do not accumulate handles)."""
@@ -230,21 +245,22 @@ def batch_reactor(input_file, lib_dir, udf=None, *, sens=False, surfchem=False, 
     finally:
         for s in streams:
             s.close()
-    return "Success" if st["status"][0] == 0 else "Failure"
+    return retcode(st["status"][0])
 
 
 def batch_reactor_programmatic(inlet_comp, T, p, time, *, Asv=1.0, chem: Chemistry, mech: Mechanism, device=0):
     """batch_reactor(inlet_comp, T, p, time; Asv, chem, thermo_obj, md) (src/BatchReactor.jl:86-147).
     Returns (t, Dict(species => x_end)) with t = [0, time] (save_everystep=false). Species are
     matched by name, so the Julia Dict key order of the surface case (species =
-    collect(keys(inlet_comp)), :103) does not change the result."""
+    collect(keys(inlet_comp)), :103) does not change the result. As the reference (which does not
+    check sol.retcode here), a failed integration still returns: t ends at the time reached and x is
+    that of the last accepted state (batch_reactor_ensemble returns the status codes)."""
     x = mech.mole_fractions(inlet_comp)
     u0 = mech.initial_state(T, p, x)
     u, st = _engine(mech, device).integrate([T], [Asv], u0[None, :], [time])
-    if st["status"][0] != 0:
-        raise RuntimeError(f"integration failed with status {st['status'][0]}")
+    t_end = float(time) if st["status"][0] == 0 else float(st["t_end"][0])
     xf = mech.state_to_molefrac(u[0])
-    return [0.0, float(time)], dict(zip(mech.gas_species, xf))
+    return [0.0, t_end], dict(zip(mech.gas_species, xf))
 
 
 def batch_reactor_ensemble(mech: Mechanism, T, p, X, time, *, Asv=1.0, theta0=None, device=0, rtol=1e-6,

@@ -14,7 +14,13 @@ Scaling (BASELINE.json: "ensemble of 1e5 reactors, sharded over 1/2/4/8 GPUs"):
   --scaling weak:             every rank integrates N reactors (--n).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config gri|h2o2|surf|gas_surf]
-                  [--scaling strong|weak] [--n N] [--no-cpu] [--no-phase]
+                  [--scaling strong|weak] [--n N] [--no-cpu] [--no-phase] [--dry-run]
+
+Launch: under torch.distributed.run (WORLD_SIZE set) every process is one rank. Without a launcher,
+--gpus N > 1 makes this process spawn N rank processes (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
+127.0.0.1) before it touches any GPU, wait for them and exit with the first non-zero status; a rank
+whose process group reports another world size than --gpus exits non-zero. --dry-run runs the same
+launch and sharding over gloo on the CPU without touching a GPU (tests/test_shard.py).
 """
 import argparse
 import json
@@ -63,20 +69,34 @@ def main():
     ap.add_argument("--no-phase", action="store_true", help="skip the rate+Jacobian phase split (diag build)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive extra step (counter runs: "
                                                           "one integrator dispatch per timed step only)")
+    ap.add_argument("--dry-run", action="store_true", help="launch + sharding over gloo, no GPU (CPU test)")
     ap.add_argument("--phase-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.phase_only:
         return phase_split(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)   # (no torch import, no GPU call in this process)
 
     import torch
     import torch.distributed as dist
-    import _pkgload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, dist, world, rank)
+    import _pkgload
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:   # the line's n_gpus is the world RCCL reports
+            print(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks",
+                  file=sys.stderr)
+            dist.destroy_process_group()
+            return 2
+        world = dist.get_world_size()
+    elif args.gpus != 1:
+        print(f"bench.py: --gpus {args.gpus} with WORLD_SIZE=1", file=sys.stderr)
+        return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -258,6 +278,60 @@ def main():
         dist.destroy_process_group()
 
 
+def spawn_ranks(n):
+    """One child process per rank (the driver's torch.distributed.run launch, done here): each gets
+    RANK = LOCAL_RANK = r, WORLD_SIZE = n and a 127.0.0.1 rendezvous, runs this script with the same
+    arguments, and rank 0 prints the line. Returns the first non-zero child status (0 if all pass)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def dry_run(args, dist, world, rank):
+    """--dry-run: the rank layout and shard slices over gloo on the CPU (no GPU, no integration);
+    rank 0 prints {"n_gpus": world size from the process group, "slices": [[start, stop], ...]}."""
+    import importlib.util   # the package's pure-Python shard module alone (no library load)
+    spec = importlib.util.spec_from_file_location("br_shard", os.path.join(ROOT, "batchreactor.jl_amd", "shard.py"))
+    shard = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(shard)
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the process group has {world} ranks", file=sys.stderr)
+            dist.destroy_process_group()
+            return 2
+    elif args.gpus != 1:
+        print(f"bench.py: --gpus {args.gpus} with WORLD_SIZE=1", file=sys.stderr)
+        return 2
+    cfg = CONFIGS[args.config]
+    if args.scaling == "strong":
+        total = args.n or cfg["n"]
+        mine = list(shard.shard_range(rank, world, total))
+    else:
+        total = (args.n or cfg["n"]) * world
+        mine = list(shard.shard_slice(rank, args.n or cfg["n"]))
+    slices = [None] * world
+    if world > 1:
+        dist.all_gather_object(slices, mine)
+        dist.destroy_process_group()
+    else:
+        slices = [mine]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": args.scaling, "total_reactors": total,
+                          "slices": slices}), flush=True)
+    return 0
+
+
 def pcie_step(torch, dist, world, dev, host_in, dev_in, dU, dst, step, gathered, shard):
     """One more step with the inputs in pinned host memory and the final states + counters copied
     back to it (PCIe-inclusive wall time, max over ranks)."""
@@ -390,4 +464,4 @@ def cpu_baseline(mech, config, T, Asv, U0, tf, U_gpu, gpu_status, seconds, eng):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

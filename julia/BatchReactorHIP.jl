@@ -306,7 +306,21 @@ function batch_reactor(input_file::AbstractString, lib_dir::AbstractString; sens
     end
     _write_profiles(dirname(abspath(input_file)), dm, surfchem, inp.T, trace, nst)
     _free!(dm)
-    return stats[8, 1] == 0 ? Symbol("Success") : Symbol("Failure")
+    return retcode_symbol(stats[8, 1])
+end
+
+"""Symbol(sol.retcode) of the reference's CVODE_BDF solve (src/BatchReactor.jl:216) for an engine status
+(include/brhip.h): as Sundials.jl's interpret_sundials_retcode, -1 (CV_TOO_MUCH_WORK) -> :MaxIters,
+-2 / -3 (CV_TOO_MUCH_ACC, CV_ERR_FAILURE) -> :Unstable, -4 (CV_CONV_FAILURE) -> :ConvergenceFailure,
+other failures -> :Failure; a NaN state (SciML's unstable_check, status -7) -> :Unstable. The same
+table as the Python host's reactor.RETCODES."""
+function retcode_symbol(status::Real)
+    s = Int(status)
+    s == 0 && return :Success
+    s == -1 && return :MaxIters
+    (s == -2 || s == -3 || s == -7) && return :Unstable
+    s == -4 && return :ConvergenceFailure
+    return :Failure
 end
 
 """residual!(du, u, p, t) (src/BatchReactor.jl:312-376) of one reactor on the GPU (br_rhs)."""
@@ -496,6 +510,6 @@ function batch_reactor(input_file::AbstractString, lib_dir::AbstractString, user
 end
 
 export batch_reactor, batch_reactor_ensemble, compile_mechanism, read_batch_xml, DeviceMech, Chemistry,
-       UserDefinedState, BrOpts
+       UserDefinedState, BrOpts, retcode_symbol
 
 end # module

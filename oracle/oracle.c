@@ -608,7 +608,13 @@ static double g_rop_jitter = 0.0;
 /* per thread, and touched only while the jitter is on: a shared counter written by every OpenMP thread on
  * every RHS call was a data race and put all threads on one cache line (16-thread baseline -80 %, r04) */
 static _Thread_local unsigned long long g_rop_calls = 0;
+/* deterministic streams: each integration restarts the counter at (seed, reactor index) << 24, so a
+ * reactor's jitter sequence does not depend on the thread that ran it or on what that thread ran
+ * before (orc_integrate_batch passes the batch index; single integrations use index 0) */
+static unsigned long long g_rop_seed = 0;
+static _Thread_local unsigned long long g_rop_reactor = 0;
 void orc_set_rop_jitter(double eps) { g_rop_jitter = eps; }
+void orc_set_rop_jitter_seed(unsigned long long seed) { g_rop_seed = seed; }
 static inline double rop_jit(int i) {
     unsigned long long h = (g_rop_calls * 0x9E3779B97F4A7C15ull) ^ ((unsigned long long)i * 0xC2B2AE3D27D4EB4Full);
     h ^= h >> 31;
@@ -1404,6 +1410,7 @@ static int integrate_impl(const orc_mech* m, double T, double Asv, double* u, do
                           const orc_opts* o, orc_stats* st, orc_step_cb cb, void* user,
                           int nout, const double* tout, double* yout) {
     tcache_t tc; tcache_init(m, T, &tc);
+    g_rop_calls = ((g_rop_seed << 20) + g_rop_reactor) << 24;
     cv_t cvs; cv_t* cv = &cvs; memset(cv, 0, sizeof *cv);
     int n = m->ng + m->ns;
     cv->m = m; cv->tc = &tc; cv->Asv = Asv; cv->n = n;
@@ -1508,8 +1515,10 @@ int orc_integrate_batch_out(const orc_mech* m, int N, const double* T, const dou
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : bad)
 #endif
     for (int i = 0; i < N; ++i) {
+        g_rop_reactor = (unsigned long long)i;
         int r = integrate_impl(m, T[i], Asv ? Asv[i] : 1.0, u + (size_t)i * n, tf[i], o, st ? &st[i] : NULL, NULL, NULL,
                                nout, tout, yout ? yout + (size_t)i * nout * n : NULL);
+        g_rop_reactor = 0;
         if (r) bad++;
     }
     (void)nthreads;

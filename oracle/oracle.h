@@ -110,6 +110,7 @@ int  orc_integrate_out(const orc_mech* m, double T, double Asv, double* u, doubl
                        orc_stats* st, int nout, const double* tout, double* yout);
 /* diagnostic: perturb every rate of progress by a relative +-eps (0 = off; not thread-safe) */
 void orc_set_rop_jitter(double eps);
+void orc_set_rop_jitter_seed(unsigned long long seed);   /* jitter realisation (streams per reactor index) */
 /* diagnostic: pivot-order statistics of the factorizations (this thread; orc_lu_diag(1) resets and
  * enables): out4 = factorizations, those whose pivot order differs from the previous one's, steps,
  * row interchanges needed when the rows are loaded in the previous pivot order, sum of their steps,

@@ -89,6 +89,8 @@ def lib():
         L.orc_integrate_batch_out.restype = C.c_int
         L.orc_set_rop_jitter.argtypes = [C.c_double]
         L.orc_set_rop_jitter.restype = None
+        L.orc_set_rop_jitter_seed.argtypes = [C.c_ulonglong]
+        L.orc_set_rop_jitter_seed.restype = None
         _lib = L
     return _lib
 

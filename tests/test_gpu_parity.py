@@ -351,9 +351,10 @@ def test_batched_lu_solve(pkg, gpu, n):
 @pytest.mark.parametrize("n", [33, 53, 64])
 def test_batched_lu_solve_mfma(pkg, gpu, n):
     """The MFMA-blocked LU (lu_factor_mf: 8-column panels, trailing updates X += E' X[piv] on
-    v_mfma_f64_16x16x4f64; not the integrator's default, see profiles/r04_lu_mfma_ab.json) + solve,
-    the same matrices and backward-error bound as test_batched_lu_solve; factored twice (natural
-    row order, then the first factorization's pivot order)."""
+    v_mfma_f64_16x16x4f64; measured slower in the integrator, profiles/r04_lu_mfma_ab.json, so it
+    lives in the variant library libbrhip_lumf.so, not in libbrhip.so) + the product's solve, the
+    same matrices and backward-error bound as test_batched_lu_solve; factored twice (natural row
+    order, then the first factorization's pivot order)."""
     import ctypes as C
     rng = np.random.default_rng(n)
     N = 64
@@ -362,8 +363,9 @@ def test_batched_lu_solve_mfma(pkg, gpu, n):
     b = rng.standard_normal((N, n))
     x = np.zeros((N, n))
     f = np.zeros(N, np.int32)
-    L = pkg._lib.lib()
-    fn = L.br_debug_lu_solve_mf
+    path = os.path.join(os.path.dirname(pkg._lib.__file__), "libbrhip_lumf.so")
+    assert os.path.exists(path), "variant library not built (make -C batchreactor.jl_amd/csrc)"
+    fn = C.CDLL(path).br_debug_lu_solve_mf
     fn.restype = C.c_int
     rc = fn(N, n, pkg._lib.dptr(J), pkg._lib.dptr(g), pkg._lib.dptr(b), pkg._lib.dptr(x),
             f.ctypes.data_as(C.POINTER(C.c_int)))
@@ -476,8 +478,9 @@ def test_file_driven_gas_surf_profiles(pkg, gpu, tmp_path):
 def test_reference_file_scenarios(pkg, orc, gpu, tmp_path, scenario, chem):
     """The reference's file-driven testsets (test/runtests.jl:13-29: surface, H2/O2 = config C1,
     GRI CH4) through batch_reactor on the GPU: "Success", the four output files, the last row at
-    t = tf, and the final state against the oracle's run of the same input (CVODE's DQ Jacobian
-    for the lane engine, analytic for the wavefront engine): species >= 1e-6 to 1e-3 relative."""
+    t = tf, and the final state against the oracle's run of the same input (the file path traces its
+    rows, so it runs on the wavefront engine with the analytic Jacobian, and the oracle uses the
+    analytic Jacobian too): species >= 1e-6 to 1e-3 relative."""
     import csv
     import shutil
     from conftest import GOLDEN

@@ -299,3 +299,24 @@ def test_cli_julia_string_format(pkg):
     cli = os.path.join(ROOT, "batchreactor.jl_amd", "brhip_batch")
     out = subprocess.run([cli, "--fmt"], input="\n".join(toks), capture_output=True, text=True, check=True).stdout.split()
     assert out == toks
+
+
+def test_retcode_symbols(pkg):
+    """Engine status -> Symbol(sol.retcode) of the reference's CVODE_BDF solve (src/BatchReactor.jl:216),
+    one case per status code the engine returns (include/brhip.h), the same table as the Julia host's
+    retcode_symbol (checked there by text in test_julia_binding)."""
+    from batchreactor_amd import reactor
+    want = {0: "Success", -1: "MaxIters", -3: "Unstable", -4: "ConvergenceFailure", -7: "Unstable",
+            -10: "Failure", -20: "Failure", -30: "Failure"}
+    for status, sym in want.items():
+        assert reactor.retcode(status) == sym
+        assert reactor.retcode(float(status)) == sym   # stats arrive as doubles
+    jl = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "julia",
+                           "BatchReactorHIP.jl")).read()
+    body = jl[jl.index("function retcode_symbol"):]
+    body = body[:body.index("\nend")]
+    for status, sym in want.items():
+        if sym in ("Success", "MaxIters", "ConvergenceFailure"):
+            assert f":{sym}" in body
+    assert "s == -4 && return :ConvergenceFailure" in body and "s == -1 && return :MaxIters" in body
+    assert "(s == -2 || s == -3 || s == -7) && return :Unstable" in body and "return :Failure" in body

@@ -116,3 +116,33 @@ def test_two_rank_gloo_strong_scaling(pkg, orc, tmp_path):
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f"SU{r}.npy"), U)
         np.testing.assert_array_equal(np.load(tmp_path / f"SS{r}.npy"), S)
+
+
+def _bench(*args, env_extra=None):
+    import json
+    import subprocess
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_spawns_ranks_for_gpus_n():
+    """bench.py --gpus 2 without a launcher spawns two rank processes itself (before any GPU call);
+    the dry-run path runs the same launch and sharding over gloo on the CPU: n_gpus is the world
+    size the process group reports, and the two contiguous slices split the 1e5 GRI ensemble."""
+    rc, line, err = _bench("--gpus", "2", "--dry-run")
+    assert rc == 0, err
+    assert line["n_gpus"] == 2 and line["total_reactors"] == 100000
+    assert line["slices"] == [[0, 50000], [50000, 100000]]
+    rc, line, err = _bench("--gpus", "2", "--dry-run", "--scaling", "weak", "--n", "1000")
+    assert rc == 0 and line["slices"] == [[0, 1000], [1000, 2000]]
+
+
+def test_bench_rejects_world_size_mismatch():
+    """--gpus N that disagrees with the launcher's world size exits non-zero (no line printed)."""
+    rc, line, _ = _bench("--gpus", "2", "--dry-run", env_extra={"WORLD_SIZE": "1"})
+    assert rc != 0 and line is None
