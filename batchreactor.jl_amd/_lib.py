@@ -48,7 +48,13 @@ class BatchInput(C.Structure):
 EXPORTS = ["br_version", "br_last_error", "br_device_count", "br_mech_create", "br_mech_destroy", "br_mech_info", "br_mech_engine", "br_mech_launch_info",
            "br_rates", "br_rhs", "br_jacobian", "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev",
            "br_last_kernel_ms", "br_debug_lu_solve", "br_mech_parse", "br_host_mech_desc", "br_host_mech_sizes",
-           "br_host_mech_species", "br_host_mech_theta0", "br_host_mech_free", "br_mech_compile", "br_read_batch_xml"]
+           "br_host_mech_species", "br_host_mech_theta0", "br_host_mech_free", "br_mech_compile", "br_read_batch_xml",
+           "br_integrate_host"]
+
+# br_integrate_host callbacks: int f(void* user, double t, const double* u, double* du);
+# void cb(void* user, double t, const double* u)
+RHS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double))
+STEP_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_double, C.POINTER(C.c_double))
 
 _lib = None
 
@@ -89,10 +95,12 @@ def lib():
     L.br_host_mech_free.argtypes = [vp]
     L.br_mech_compile.argtypes = [cs, cs, cs, cs, C.c_int, C.c_int, C.POINTER(vp)]
     L.br_read_batch_xml.argtypes = [cs, C.POINTER(BatchInput)]
+    L.br_integrate_host.argtypes = [C.c_int, RHS_FN, vp, dp, C.c_double, C.c_double, C.c_double, C.c_int, STEP_FN, vp,
+                                    dp]
     for f in ("br_mech_create", "br_mech_destroy", "br_mech_info", "br_rates", "br_rhs", "br_jacobian",
               "br_integrate", "br_integrate_traced", "br_integrate_multi", "br_integrate_dev", "br_last_kernel_ms",
               "br_mech_parse", "br_host_mech_desc", "br_host_mech_sizes", "br_host_mech_species",
-              "br_host_mech_theta0", "br_host_mech_free", "br_mech_compile", "br_read_batch_xml"):
+              "br_host_mech_theta0", "br_host_mech_free", "br_mech_compile", "br_read_batch_xml", "br_integrate_host"):
         getattr(L, f).restype = C.c_int
     _lib = L
     return L
@@ -109,3 +117,38 @@ def dptr(a):
 
 def iptr(a):
     return a.ctypes.data_as(ip)
+
+
+def integrate_host(f, u0, tf, rtol=1e-6, atol=1e-10, max_steps=100000, on_step=None):
+    """br_integrate_host: CVODE_BDF (the engine's CVODE 5.x restatement, DQ Jacobian) on the CPU with
+    a Python right-hand side f(t, u) -> du; on_step(t, u) after every accepted step and at t = 0 / tf
+    (save_data's rows). Returns (status, u_end, stats[BR_NSTAT]). An exception in f ends the solve
+    with BR_ERR_RHS and is re-raised here."""
+    import numpy as np
+    u = np.array(u0, dtype=np.float64)
+    n = len(u)
+    err = []
+
+    def rhs(_user, t, up, dup):
+        try:
+            du = np.asarray(f(t, np.ctypeslib.as_array(up, (n,)).copy()), dtype=np.float64)
+            np.ctypeslib.as_array(dup, (n,))[:] = du
+            return 0
+        except BaseException as e:   # noqa: BLE001  (handed back after the C solver returns)
+            err.append(e)
+            return 1
+
+    def step(_user, t, up):
+        if on_step is not None and not err:
+            try:
+                on_step(t, np.ctypeslib.as_array(up, (n,)).copy())
+            except BaseException as e:   # noqa: BLE001
+                err.append(e)
+
+    st = np.zeros(NSTAT)
+    fr, fs = RHS_FN(rhs), STEP_FN(step)   # (kept alive for the call)
+    status = lib().br_integrate_host(n, fr, None, dptr(u), float(tf), float(rtol), float(atol), int(max_steps), fs,
+                                     None, dptr(st))
+    if err:
+        raise err[0]
+    return status, u, st

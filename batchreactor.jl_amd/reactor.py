@@ -175,12 +175,14 @@ def _gpu_rhs_problem(mech, eng, T, Asv, u0, tf, chem):
     return params, ODEProblem(residual, u0, t_span, params), t_span
 
 
-def _udf_run(mech, x0, T, p0, tf, chem, folder, progress):
+def _udf_run(mech, x0, T, p0, tf, chem, folder, progress, max_steps=100000):
     """userchem path (src/BatchReactor.jl:197-200,:358-360,:371-372): the user's host function fills
     state.source; du = source .* molwt. As in the reference, the state handed to the udf keeps the
-    inlet T, p and mole fractions (residual! never updates u_state). Host code by nature: it is
-    integrated with SciPy's BDF on the host and is not part of the GPU hot path."""
-    from scipy.integrate import solve_ivp
+    inlet T, p and mole fractions (residual! never updates u_state). The reference solves it with
+    CVODE_BDF() (:204-210); a Python function cannot run in a kernel, so it is integrated on the CPU
+    by br_integrate_host -- the engine's CVODE 5.x restatement with CVODE's DQ Jacobian, the same solver
+    the Julia host calls -- with one save_data row per accepted step (:383-402)."""
+    from . import _lib
     ng = mech.ng
     state = UserDefinedState(T, p0, np.array(x0, float), mech.molwt, list(mech.gas_species), np.zeros(ng))
     u0 = mech.initial_state(T, p0, x0)
@@ -189,15 +191,15 @@ def _udf_run(mech, x0, T, p0, tf, chem, folder, progress):
         chem.udf(state)
         return np.asarray(state.source[:ng], float) * mech.molwt
 
-    sol = solve_ivp(f, (0.0, tf), u0, method="BDF", rtol=1e-6, atol=1e-10)
     streams = _open_streams(folder, mech, False)
     try:
-        for k in range(len(sol.t)):
-            _row(streams, False, sol.t[k], T, state.p, float(np.sum(sol.y[:ng, k])), state.mole_frac, (), progress)
+        status, _, _ = _lib.integrate_host(
+            f, u0[:ng], tf, max_steps=max_steps,
+            on_step=lambda t, u: _row(streams, False, t, T, state.p, float(np.sum(u)), state.mole_frac, (), progress))
     finally:
         for s in streams:
             s.close()
-    return "Success" if sol.success and sol.t[-1] == tf else "Failure"
+    return retcode(status)
 
 
 def batch_reactor(input_file, lib_dir, udf=None, *, sens=False, surfchem=False, gaschem=False, device=0,
@@ -220,7 +222,7 @@ def batch_reactor(input_file, lib_dir, udf=None, *, sens=False, surfchem=False, 
             params = dict(s_state=None, g_state=None, u_state=state, thermo=mech, smd=None, gmd=None,
                           cp=ConstantParams(Asv, T), chem=chem)
             return params, ODEProblem(residual, u0, (0.0, tf), params), (0.0, tf)
-        return _udf_run(mech, x, T, p0, tf, chem, folder, progress)
+        return _udf_run(mech, x, T, p0, tf, chem, folder, progress, max_steps)
     eng = _engine(mech, device)
     if sens:
         return _gpu_rhs_problem(mech, eng, T, Asv, u0, tf, chem)

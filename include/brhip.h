@@ -38,6 +38,7 @@ extern "C" {
 #define BR_ERR_CONV      -4   /* CVODE CV_CONV_FAILURE    */
 #define BR_ERR_UNSTABLE  -7   /* NaN state (SciML ReturnCode.Unstable), or the opt-in runaway test of
                                  br_opts.unstable_factor */
+#define BR_ERR_RHS       -8   /* CVODE CV_RHSFUNC_FAIL: a br_integrate_host right-hand side returned != 0 */
 #define BR_ERR_INPUT    -10
 #define BR_ERR_HIP      -20
 #define BR_ERR_UNSUPPORTED -30
@@ -227,6 +228,19 @@ int br_integrate_dev(br_mech* m, int N, const double* dT, const double* dAsv, do
 /* dense-solver check (tests): factor I - gamma_i*J_i with the engine's batched LU and solve
  * x_i = (I - gamma_i J_i)^-1 b_i. J[N][n][n] row-major; fail[i] = 0 or (k+1) for a zero pivot. */
 int br_debug_lu_solve(int N, int n, const double* J, const double* gamma, const double* b, double* x, int* fail);
+
+/* User-defined chemistry: replaces solve(ODEProblem(residual!, u0, (0, tf), params), CVODE_BDF();
+ * reltol, abstol, save_everystep=false, callback=FunctionCallingCallback(save_data)) with the userchem
+ * residual! (src/BatchReactor.jl:51-54,:197-200,:204-210,:358-360,:371-372). The user's RHS is host
+ * code (a Julia or Python function: it cannot run in a kernel), so this runs on the CPU: the same
+ * CVODE 5.x restatement as the engine, with CVODE's DQ Jacobian (the reference supplies none).
+ * f(user, t, u, du) returns 0 (non-zero ends the solve with BR_ERR_RHS); cb(cb_user, t, u) after every
+ * accepted step and at t = 0 and t = tf (save_data's rows). u: u0 in, u(tf) out (the last accepted
+ * state on failure); stats[BR_NSTAT] as br_stats. Returns 0 or a BR_ERR_* status. No GPU. */
+typedef int (*br_rhs_fn)(void* user, double t, const double* u, double* du);
+typedef void (*br_step_fn)(void* user, double t, const double* u);
+int br_integrate_host(int n, br_rhs_fn f, void* user, double* u, double tf, double rtol, double atol, int max_steps,
+                      br_step_fn cb, void* cb_user, double* stats);
 
 /* timing helper for roofline accounting: duration (ms) of the last integrate kernel,
  * measured with HIP events on the stream it was launched on (after the stream syncs). */

@@ -403,55 +403,50 @@ mutable struct UserDefinedState
     source::Vector{Float64}
 end
 
-"""One adaptive step sequence of the Dormand-Prince 5(4) pair (FSAL, WRMS error norm with the
-reference's tolerances) for du/dt = f(t) on the host. In the reference's userchem path residual!
-never updates the state the udf sees (u_state keeps the inlet T, p and mole fractions, :358-360), so
-the source cannot depend on u: the ODE is a quadrature, not stiff. Calls `rowcb(t, u)` after every
-accepted step (save_data's callback, :208-210) and returns (t_end, u, success)."""
-function _dopri_host(f!, u0::Vector{Float64}, tf::Float64; rtol=1e-6, atol=1e-10, max_steps=100_000,
-                     rowcb=(t, u) -> nothing)
-    c = (0.0, 1/5, 3/10, 4/5, 8/9, 1.0, 1.0)
-    a = ((), (1/5,), (3/40, 9/40), (44/45, -56/15, 32/9), (19372/6561, -25360/2187, 64448/6561, -212/729),
-         (9017/3168, -355/33, 46732/5247, 49/176, -5103/18656), (35/384, 0.0, 500/1113, 125/192, -2187/6784, 11/84))
-    e = (71/57600, 0.0, -71/16695, 71/1920, -17253/339200, 22/525, -1/40)   # b5 - b4
-    n = length(u0)
-    u = copy(u0)
-    k = [zeros(n) for _ in 1:7]
-    t = 0.0
-    f!(k[1], u, t)
-    h = tf > 0 ? min(tf, 1e-6 * max(tf, 1.0)) : 0.0
-    rowcb(t, u)
-    nst = 0
-    while t < tf
-        nst >= max_steps && return t, u, false
-        h = min(h, tf - t)
-        for s in 2:7
-            y = copy(u)
-            for j in 1:(s - 1)
-                y .+= h * a[s][j] .* k[j]
-            end
-            f!(k[s], y, t + c[s] * h)
-        end
-        unew = copy(u)
-        for j in 1:6
-            unew .+= h * a[7][j] .* k[j]
-        end
-        err = zeros(n)
-        for j in 1:7
-            err .+= h * e[j] .* k[j]
-        end
-        w = atol .+ rtol .* max.(abs.(u), abs.(unew))
-        en = sqrt(sum((err ./ w) .^ 2) / max(n, 1))
-        if en <= 1.0 || h <= 16 * eps(max(abs(t), 1.0))
-            t = (tf - t - h <= 16 * eps(max(abs(tf), 1.0))) ? tf : t + h
-            u = unew
-            k[1] .= k[7]                                                   # FSAL
-            nst += 1
-            rowcb(t, u)
-        end
-        h *= en == 0 ? 5.0 : clamp(0.9 * en^(-1 / 5), 0.2, 5.0)
+mutable struct _HostCtx
+    n::Int
+    f!::Any          # f!(du, u, t)
+    rowcb::Any       # rowcb(t, u)
+    err::Any
+end
+
+# br_integrate_host callbacks: the user's residual! and save_data's row per accepted step
+function _host_rhs(user::Ptr{Cvoid}, t::Cdouble, u::Ptr{Cdouble}, du::Ptr{Cdouble})::Cint
+    ctx = unsafe_pointer_to_objref(user)::_HostCtx
+    try
+        ctx.f!(unsafe_wrap(Array, du, ctx.n), copy(unsafe_wrap(Array, u, ctx.n)), t)
+        return Cint(0)
+    catch e
+        ctx.err = e
+        return Cint(1)                                                  # -> BR_ERR_RHS
     end
-    return t, u, true
+end
+function _host_step(user::Ptr{Cvoid}, t::Cdouble, u::Ptr{Cdouble})::Cvoid
+    ctx = unsafe_pointer_to_objref(user)::_HostCtx
+    ctx.err === nothing && ctx.rowcb(t, copy(unsafe_wrap(Array, u, ctx.n)))
+    return nothing
+end
+
+"""CVODE_BDF() on the host with a Julia right-hand side f!(du, u, t) (br_integrate_host: the engine's
+CVODE 5.x restatement with CVODE's DQ Jacobian, the reference's setting, src/BatchReactor.jl:204-210;
+the same solver the Python host's udf path calls). rowcb(t, u) after every accepted step and at
+t = 0 / tf (save_data's rows, :208). Returns (status, u_end, stats); an exception in f! is rethrown."""
+function integrate_host(f!, u0::Vector{Float64}, tf::Float64; rtol=1e-6, atol=1e-10, max_steps=100_000,
+                        rowcb=(t, u) -> nothing)
+    ctx = _HostCtx(length(u0), f!, rowcb, nothing)
+    u = copy(u0)
+    stats = zeros(NSTAT)
+    frhs = @cfunction(_host_rhs, Cint, (Ptr{Cvoid}, Cdouble, Ptr{Cdouble}, Ptr{Cdouble}))
+    fstep = @cfunction(_host_step, Cvoid, (Ptr{Cvoid}, Cdouble, Ptr{Cdouble}))
+    status = GC.@preserve ctx begin
+        p = pointer_from_objref(ctx)
+        ccall((:br_integrate_host, lib), Cint,
+              (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float64}, Cdouble, Cdouble, Cdouble, Cint, Ptr{Cvoid}, Ptr{Cvoid},
+               Ptr{Float64}),
+              length(u0), frhs, p, u, tf, rtol, atol, max_steps, fstep, p, stats)
+    end
+    ctx.err === nothing || throw(ctx.err)
+    return status, u, stats
 end
 
 """batch_reactor(input_file, lib_dir, user_defined::Function; sens=false) (src/BatchReactor.jl:51-54):
@@ -459,9 +454,10 @@ user-defined chemistry. The gas species are batch.xml's <gasphase> (no mechanism
 molecular weights from lib_dir/therm.dat through br_mech_parse, no GPU). The udf is called with a
 UserDefinedState whose T, p and mole fractions stay at the inlet values, as in the reference; its
 `source` drives du = source .* molwt. Host code by nature (a Julia callback cannot run in a HIP
-kernel): integrated on the host (_dopri_host), one output row per accepted step in the save_data
-format (t, T, p, rho = sum(u), the state's mole fractions; :383-402). sens=true returns
-(params, prob, t_span) with prob.f = residual! (:205-207)."""
+kernel): integrated by CVODE_BDF on the host (integrate_host -> br_integrate_host, as the reference's
+solve at :204-210), one output row per accepted step in the save_data format (t, T, p, rho = sum(u),
+the state's mole fractions; :383-402). Returns Symbol(retcode). sens=true returns (params, prob, t_span)
+with prob.f = residual! (:205-207)."""
 function batch_reactor(input_file::AbstractString, lib_dir::AbstractString, user_defined::Function;
                        sens::Bool=false, max_steps::Integer=100_000)
     inp = read_batch_xml(input_file)
@@ -491,7 +487,7 @@ function batch_reactor(input_file::AbstractString, lib_dir::AbstractString, user
     s_dat = open(joinpath(folder, "surface_covg.dat"), "w")
     g_csv = open(joinpath(folder, "gas_profile.csv"), "w")
     s_csv = open(joinpath(folder, "surface_covg.csv"), "w")
-    ok = false
+    status = 0
     try
         hdr = vcat(["t", "T", "p", "rho"], names)
         write(g_dat, join([@sprintf("%10s\t", hh) for hh in hdr]), "\n")
@@ -502,14 +498,14 @@ function batch_reactor(input_file::AbstractString, lib_dir::AbstractString, user
             write(g_csv, join(string.(vals), ","), "\n")
         end
         f! = (du, u, t) -> residual!(du, u, nothing, t)
-        _, _, ok = _dopri_host(f!, u0, Float64(inp.time); max_steps=max_steps, rowcb=row)
+        status, _, _ = integrate_host(f!, u0, Float64(inp.time); max_steps=max_steps, rowcb=row)
     finally
         close(g_dat); close(s_dat); close(g_csv); close(s_csv)
     end
-    return ok ? Symbol("Success") : Symbol("MaxIters")
+    return retcode_symbol(status)
 end
 
 export batch_reactor, batch_reactor_ensemble, compile_mechanism, read_batch_xml, DeviceMech, Chemistry,
-       UserDefinedState, BrOpts, retcode_symbol
+       UserDefinedState, BrOpts, retcode_symbol, integrate_host
 
 end # module

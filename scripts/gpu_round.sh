@@ -19,6 +19,7 @@ STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *tests* ]] && run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 [[ $STEPS == *bench* ]] && run bench 900 python3 bench.py ${BENCH_ARGS:-}
+[[ $STEPS == *parity* ]] && run parity 1200 python3 -u scripts/parity_outliers.py ${PARITY_ARGS:-}
 [[ $STEPS == *prof* ]] && run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${PROF_ARGS:---steps 3 --warmup 1}
 if [[ $STEPS == *pmc* ]]; then   # HBM traffic of k_integrate: separate counter passes (no tracing)
   PN=${PMC_N:-20000}

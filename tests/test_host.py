@@ -320,3 +320,46 @@ def test_retcode_symbols(pkg):
             assert f":{sym}" in body
     assert "s == -4 && return :ConvergenceFailure" in body and "s == -1 && return :MaxIters" in body
     assert "(s == -2 || s == -3 || s == -7) && return :Unstable" in body and "return :Failure" in body
+
+
+@pytest.mark.parametrize("mech_file,T,x", [("h2o2.dat", 1173.0, {"H2": 0.25, "O2": 0.25, "N2": 0.5}),
+                                           ("grimech.dat", 1200.0, {"CH4": 0.25, "O2": 0.5, "N2": 0.25})])
+def test_host_cvode_matches_oracle_dq(pkg, orc, mech_file, T, x):
+    """br_integrate_host (the udf path's solver: CVODE 5.x on the CPU with a caller's RHS and CVODE's DQ
+    Jacobian, src/BatchReactor.jl:204-210) driven by the oracle's own residual! through the ctypes
+    callback, against the oracle's integration of the same problem with the DQ Jacobian: the same
+    algorithm, so the same accepted steps, counters and end state (to rounding: the two are compiled
+    separately). Also the save_data rows: one per accepted step plus t = 0."""
+    from batchreactor_amd import _lib
+    om = orc.Mech(os.path.join(LIB, mech_file), os.path.join(LIB, "therm.dat"))
+    m = pkg.Mechanism.from_files(LIB, gas_mech=mech_file)
+    u0 = m.initial_state(T, 1e5, m.mole_fractions(x))
+    tf = 1e-2
+    rows = []
+    status, u, st = _lib.integrate_host(lambda t, u: om.rhs(T, 1.0, u)[0], u0, tf,
+                                        on_step=lambda t, u: rows.append((t, u)))
+    uo, so, _ = om.integrate(T, 1.0, u0, tf, analytic_jac=False)
+    assert status == 0 and so["status"] == 0
+    assert int(st[0]) == so["nsteps"] and int(st[2]) == so["nje"] and int(st[3]) == so["nsetups"]
+    assert int(st[1]) == so["nfe"] and int(st[4]) == so["nni"] and int(st[19]) == so["nfeDQ"]
+    np.testing.assert_allclose(u, uo, rtol=1e-12, atol=1e-22)
+    assert len(rows) == so["nsteps"] + 1 and rows[0][0] == 0.0 and rows[-1][0] == tf
+
+
+def test_host_cvode_status_codes(pkg):
+    """br_integrate_host's failure paths and their SciML retcodes: a step limit -> MaxIters, a NaN
+    right-hand side -> Unstable-class failure, an exception in the RHS -> re-raised, bad input -> -10."""
+    from batchreactor_amd import _lib, reactor
+    f = lambda t, u: -1e3 * (u - np.array([1.0, 2.0]))   # noqa: E731  (stiff linear relaxation)
+    status, u, st = _lib.integrate_host(f, [0.0, 0.0], 10.0)
+    assert status == 0 and np.allclose(u, [1.0, 2.0], rtol=1e-5)
+    status, _, st = _lib.integrate_host(f, [0.0, 0.0], 10.0, max_steps=5)
+    assert status == -1 and int(st[0]) == 5 and reactor.retcode(status) == "MaxIters"
+    status, _, _ = _lib.integrate_host(lambda t, u: np.full(2, np.nan), [1.0, 1.0], 1.0)
+    assert status < 0 and reactor.retcode(status) != "Success"
+
+    def boom(t, u):
+        raise ValueError("udf failed")
+    with pytest.raises(ValueError):
+        _lib.integrate_host(boom, [1.0], 1.0)
+    assert _lib.integrate_host(f, [0.0, 0.0], -1.0)[0] == -10

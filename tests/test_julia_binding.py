@@ -136,6 +136,7 @@ _ARG = {
     "const br_opts*": {"Ref{BrOpts}", "Ptr{BrOpts}"},
     "br_stats*": {"Ptr{Float64}"},   # [NSTAT x N] Float64: br_stats is BR_NSTAT doubles
     "br_batch_input*": {"Ref{BrBatchInput}"}, "void*": {"Ptr{Cvoid}"},
+    "br_rhs_fn": {"Ptr{Cvoid}"}, "br_step_fn": {"Ptr{Cvoid}"},   # @cfunction pointers
 }
 _ARG = {k.replace(" ", ""): v for k, v in _ARG.items()}     # compared with all blanks removed
 _RET = {"int": "Cint", "constchar*": "Cstring"}
