@@ -261,8 +261,10 @@ def batch_reactor_programmatic(inlet_comp, T, p, time, *, Asv=1.0, chem: Chemist
     u0 = mech.initial_state(T, p, x)
     u, st = _engine(mech, device).integrate([T], [Asv], u0[None, :], [time])
     t_end = float(time) if st["status"][0] == 0 else float(st["t_end"][0])
-    xf = mech.state_to_molefrac(u[0])
-    return [0.0, t_end], dict(zip(mech.gas_species, xf))
+    xf = dict(zip(mech.gas_species, mech.state_to_molefrac(u[0])))
+    if chem.surfchem and not chem.gaschem:   # species = collect(keys(inlet_comp)) (:103, :145)
+        return [0.0, t_end], {k: xf[k.upper()] for k in inlet_comp}
+    return [0.0, t_end], xf
 
 
 def batch_reactor_ensemble(mech: Mechanism, T, p, X, time, *, Asv=1.0, theta0=None, device=0, rtol=1e-6,

@@ -349,9 +349,14 @@ function batch_reactor(inlet_comp::AbstractDict, T::Real, p::Real, time::Real; A
     end
     u = reshape(initial_state(md, T, p, inlet_comp), ncomp(md), 1)
     stats = integrate!(md.m, [Float64(T)], [Float64(Asv)], u, [Float64(time)]; opts=BrOpts(dq_jacobian=dq_jacobian))
-    stats[8, 1] == 0 || error("integration failed with status $(stats[8, 1])")
-    xf = state_to_molefrac(md, u[:, 1])
-    return [0.0, Float64(time)], Dict(zip(gas_species(md), xf))
+    # as the reference (which does not check sol.retcode here): a failed solve still returns, t ending
+    # at the time reached and x from the last accepted state
+    tend = stats[8, 1] == 0 ? Float64(time) : stats[14, 1]
+    xf = Dict(zip(gas_species(md), state_to_molefrac(md, u[:, 1])))
+    if md.nrg == 0 && md.ns > 0   # surfchem: species = collect(keys(inlet_comp)) (:103, :145)
+        return [0.0, tend], Dict(String(k) => xf[uppercase(String(k))] for k in keys(inlet_comp))
+    end
+    return [0.0, tend], xf
 end
 
 """batch_reactor_ensemble: N independent reactors, each with its own T, p, inlet composition and

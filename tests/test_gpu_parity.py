@@ -554,6 +554,7 @@ def test_surface_programmatic_species_order(pkg, gpu):
         m = pkg.Mechanism.from_files(LIB, surface_mech="ch4ni.xml", gasphase=list(c))
         t, xd = pkg.batch_reactor_programmatic(c, 1073.15, 1e5, 10, Asv=10.0, chem=pkg.Chemistry(surfchem=True), mech=m)
         assert t[-1] == 10
+        assert list(xd) == order        # the returned Dict's keys are inlet_comp's (:103, :145)
         res.append(xd)
     for xd in res[1:]:
         for k in comp:
