@@ -601,9 +601,10 @@ static void falloff(const orc_mech* m, const grxn_t* r, const tcache_t* c, int i
     *dfac = (F / ((1 + Pr) * (1 + Pr)) + F * g / (1 + Pr)) * (k0 / kinf);
 }
 
-/* diagnostic hook (scripts/diag_spread.py): every rate of progress times (1 +- eps), the sign from a
- * hash of (call, reaction) -- the few-ulp differences of an RHS implementation that evaluates the
- * same formulas in another order, amplified by CVODE's DQ Jacobian (inc ~ 1e-8 |y|). 0 = off. */
+/* diagnostic hook (scripts/parity_outliers.py, diag_spread.py): every rate of progress -- for a gas
+ * reaction each direction kf Pf, kr Pb separately -- times (1 +- eps), the sign from a hash of (call,
+ * reaction, direction): the few-ulp differences of an RHS implementation that evaluates the same
+ * formulas in another order, amplified by CVODE's DQ Jacobian (inc ~ 1e-8 |y|). 0 = off. */
 static double g_rop_jitter = 0.0;
 /* per thread, and touched only while the jitter is on: a shared counter written by every OpenMP thread on
  * every RHS call was a data race and put all threads on one cache line (16-thread baseline -80 %, r04) */
@@ -615,8 +616,10 @@ static unsigned long long g_rop_seed = 0;
 static _Thread_local unsigned long long g_rop_reactor = 0;
 void orc_set_rop_jitter(double eps) { g_rop_jitter = eps; }
 void orc_set_rop_jitter_seed(unsigned long long seed) { g_rop_seed = seed; }
-static inline double rop_jit(int i) {
-    unsigned long long h = (g_rop_calls * 0x9E3779B97F4A7C15ull) ^ ((unsigned long long)i * 0xC2B2AE3D27D4EB4Full);
+static inline double rop_jit(int i) {   /* sign from a splitmix64 finaliser of (call, reaction): every bit mixed */
+    unsigned long long h = g_rop_calls * 0x9E3779B97F4A7C15ull + (unsigned long long)(i + 1) * 0xC2B2AE3D27D4EB4Full;
+    h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
     h ^= h >> 31;
     return (h & 1) ? g_rop_jitter : -g_rop_jitter;
 }
@@ -628,7 +631,11 @@ static void gas_rop(const orc_mech* m, const tcache_t* tc, const double* c, doub
         double Pf = 1, Pb = 1;
         for (int e = 0; e < r->nf; ++e) Pf *= c[r->f[e]];
         for (int e = 0; e < r->nr; ++e) Pb *= c[r->r[e]];
-        double D = r->fmul * tc->kf[i] * Pf - r->rmul * tc->kr[i] * Pb;
+        /* jitter (diag): each direction's rate separately, so a net rate near partial equilibrium
+         * (kf Pf ~ kr Pb) carries the absolute rounding of its terms, as a reordered RHS would */
+        double D = g_rop_jitter != 0.0
+                       ? r->fmul * tc->kf[i] * Pf * (1.0 + rop_jit(2 * i)) - r->rmul * tc->kr[i] * Pb * (1.0 + rop_jit(2 * i + 1))
+                       : r->fmul * tc->kf[i] * Pf - r->rmul * tc->kr[i] * Pb;
         if (r->tb) {
             double Mc = 0;
             for (int k = 0; k < m->ng; ++k) Mc += r->eff[k] * c[k];
@@ -639,7 +646,7 @@ static void gas_rop(const orc_mech* m, const tcache_t* tc, const double* c, doub
                 if (m->conv & ORC_CONV_FALLOFF_XM) D *= Mc * 1e-6;   /* [M] in mol/cm3 */
             }
         }
-        q[i] = g_rop_jitter != 0.0 ? D * (1.0 + rop_jit(i)) : D;
+        q[i] = D;
     }
     if (g_rop_jitter != 0.0) g_rop_calls++;
 }

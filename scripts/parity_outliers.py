@@ -82,7 +82,8 @@ def calibrate(eng, om, T, A, Y, nstate=400, R=8, rng=None):
     from the oracle's by f_k - f_orc,k ~ N(0, sigma^2 s_k^2), s_k^2 = sum_r (nu_kr q_r M_k)^2. The oracle's
     jitter at eps = 4e-16 has exactly that form (random signs), so R jittered evaluations per state give
     s_k = rms_R(f_jit,k - f_orc,k) / eps; the GPU's normalised deviation e_k = |f_gpu,k - f_orc,k| / s_k
-    then estimates sigma = median(e) / 0.6745 (and p90(e) / 1.645): eps_cal = the larger of the two."""
+    then estimates sigma = median(e) / 0.6745: eps_cal (the tails, p90(e) / 1.645 and p99(e), are
+    reported beside it)."""
     rng = rng or np.random.default_rng(1)
     N, nt, n = Y.shape
     idx = rng.integers(0, N, nstate)
@@ -103,7 +104,7 @@ def calibrate(eng, om, T, A, Y, nstate=400, R=8, rng=None):
     return {"states": int(nstate), "jitter_evaluations_per_state": R, "pairs": int(m.sum()),
             "gpu_bitwise_equal_frac": float(np.mean(fg == fo)),
             "sigma_from_median": s50, "sigma_from_p90": s90, "e_p99": float(np.percentile(e, 99)),
-            "eps_cal": max(s50, s90, 1.1e-16)}
+            "eps_cal": max(s50, 1.1e-16)}
 
 
 def summarize(W):
@@ -132,10 +133,12 @@ def analyse(pkg, eng, mech, om, config, aj, K, thr, log):
         st, Y = oracle_runs(om, T, A, Up, tf, aj, thr)
         okr = oko & np.array([s["status"] == 0 for s in st])
         series.append(("u0", r, band_matrix(Y, Yo, sto, okr)))
+        log(f"    self-spread u0 #{r}: max {np.nanmax(series[-1][2], 0)}")
     for r in range(R_J):
         st, Y = oracle_runs(om, T, A, U0, tf, aj, thr, jitter=cal["eps_cal"], seed=1 + r)
         okr = oko & np.array([s["status"] == 0 for s in st])
         series.append(("jitter", r, band_matrix(Y, Yo, sto, okr)))
+        log(f"    self-spread jitter #{r}: max {np.nanmax(series[-1][2], 0)}")
     Wself = np.nanmax(np.stack([w for _, _, w in series]), axis=0)     # per reactor, max over realisations
     self_max = np.nanmax(np.stack([np.nanmax(w, 0) for _, _, w in series]), axis=0)
     proposed = [float(2 * v) for v in self_max]
@@ -143,7 +146,7 @@ def analyse(pkg, eng, mech, om, config, aj, K, thr, log):
     # outliers: beyond the current or the proposed bound
     out_idx = [i for i in np.nonzero(ok)[0] if np.any(Wg[i] > np.minimum(cur, proposed))]
     outliers = []
-    for i in out_idx[:24]:
+    for i in out_idx[:16]:
         Ti, Ai, Ui = T[i:i + 1], A[i:i + 1], U0[i:i + 1]
         own = []
         rng_i = np.random.default_rng(1000 + i)
@@ -159,7 +162,9 @@ def analyse(pkg, eng, mech, om, config, aj, K, thr, log):
         stt, Yt = oracle_runs(om, Ti, Ai, Ui, tf[i:i + 1], aj, 1, rtol=1e-10, atol=1e-16)
         _, sgt = eng.integrate(Ti, Ai, Ui, tf[i:i + 1], rtol=1e-10, atol=1e-16, tout=PB.OUT_T, dq_jacobian=not aj)
         Yg_t, Yo_t = sgt["yout"][0], Yt[0]
-        tight = float(np.max(np.abs(Yg_t - Yo_t) / (1e-6 * np.abs(Yo_t) + 1e-14)))
+        dev_t = np.abs(Yg_t - Yo_t) / (1e-6 * np.abs(Yo_t) + 1e-14)    # in 1e-6 bands, per output time
+        tight = float(np.max(dev_t))
+        tight_end = float(np.max(dev_t[-1]))                              # t = tf (the GPU test's check)
         gw = Wg[i].tolist()
         rank = [float(np.mean(own[:, w] >= gw[w])) if len(own) else None for w in range(3)]
         outliers.append({
@@ -169,15 +174,23 @@ def analyse(pkg, eng, mech, om, config, aj, K, thr, log):
             "frac_own_ge_gpu": rank,
             "t_ign_orc": float(sto[i]["t_ign"]), "t_ign_gpu": float(stg["t_ign"][i]),
             "steps_orc": int(sto[i]["nsteps"]), "steps_gpu": int(stg["nsteps"][i]),
-            "tight_rtol1e-10_max_dev_in_1e-6_bands": tight,
+            "tight_rtol1e-10_max_dev_in_1e-6_bands": tight, "tight_rtol1e-10_end_dev_in_1e-6_bands": tight_end,
             "tight_status": [int(stt[0]["status"]), int(sgt["status"][0])],
-            "verdict": ("inside the oracle's own spread" if len(own) and np.all(Wg[i] <= own.max(0) * 2)
-                        else "beyond 2x the oracle's own spread") + ("; converged runs agree to 1e-6"
-                                                                     if tight <= 1.0 else "; converged runs DIFFER"),
+            "verdict": ("inside the oracle's own spread" if len(own) and np.all(Wg[i] <= own.max(0))
+                        else "inside 2x the oracle's own spread" if len(own) and np.all(Wg[i] <= 2 * own.max(0))
+                        else "beyond 2x the oracle's own spread")
+                       + ("; converged (rtol 1e-10) end states agree to 1e-6" if tight_end <= 1.0
+                          else "; converged end states DIFFER beyond 1e-6"),
         })
         log(f"    reactor {i}: gpu {np.round(gw, 3)} own max {np.round(own.max(0), 3) if len(own) else None} "
             f"tight {tight:.3g}")
+    # bound: 2x the largest oracle self-deviation seen on these reactors -- the sample's realisations
+    # and the 32 per-reactor realisations of every examined reactor
+    own_max = np.max([o["own_spread_max"] for o in outliers if o["own_spread_max"]], axis=0) if outliers else 0 * self_max
+    bound = [float(2 * max(a, b)) for a, b in zip(self_max, own_max)]
     return {"jacobian": "analytic" if aj else "dq", "sample": int(K), "scored": int(ok.sum()),
+            "bound_rule": "2 x max(oracle self-spread over the sample's realisations, per-outlier 32-realisation spread)",
+            "bound": bound, "gpu_frac_within_bound": float(np.mean(np.all(Wg[ok] <= np.array(bound), axis=1))),
             "failed_either": int((~ok).sum()), "rhs_calibration": cal,
             "gpu_vs_oracle": summarize(Wg),
             "oracle_self_spread": {"realisations": {"u0_1e-15": R_U0, "rop_jitter_eps_cal": R_J},
