@@ -178,7 +178,7 @@ def main():
     # counted there, so it is not HBM traffic. The DRAM-destined view and the HBM bound come from
     # scripts/pmc_dram.sh -> profiles/rNN_dram_<config>.json.
     def newest(kind):
-        for rnd in ("r05", "r04", "r03", "r02"):
+        for rnd in ("r06", "r05", "r04", "r03", "r02"):
             cand = os.path.join(ROOT, "profiles", f"{rnd}_{kind}_{args.config}.json")
             if os.path.exists(cand):
                 with open(cand) as fh:
