@@ -1,4 +1,4 @@
-"""GPU lu_factor_mf (br_debug_lu_factor) against the lane-level emulation: first differing
+"""GPU lu_factor_mf (br_debug_lu_factor in the variant library libbrhip_lumf.so) against the lane-level emulation: first differing
 column of the factor matrix, per matrix. Usage (GPU box): python3 scripts/emu/cmp_lu.py [n] [twice]"""
 import ctypes as C
 import os
@@ -13,7 +13,7 @@ import _pkgload  # noqa: E402
 import lu_mf_emu as E  # noqa: E402
 
 pkg = _pkgload.load()
-L = pkg._lib.lib()
+L = C.CDLL(os.path.join(ROOT, "batchreactor.jl_amd", "libbrhip_lumf.so"))
 f = L.br_debug_lu_factor
 f.restype = C.c_int
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 53
