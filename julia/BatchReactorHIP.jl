@@ -408,6 +408,16 @@ mutable struct UserDefinedState
     source::Vector{Float64}
 end
 
+"""The state handed to the user's function: ReactionCommons.UserDefinedState when the caller has that
+package loaded (the reference's own type, built with the reference's arguments, src/BatchReactor.jl:
+197-200, so a udf annotated with it dispatches), else this module's struct with the same fields."""
+function _udf_state(T, p, x, molwt, names, source)
+    if isdefined(Main, :ReactionCommons) && isdefined(getfield(Main, :ReactionCommons), :UserDefinedState)
+        return getfield(getfield(Main, :ReactionCommons), :UserDefinedState)(T, p, x, molwt, names, source)
+    end
+    return UserDefinedState(T, p, x, molwt, names, source)
+end
+
 mutable struct _HostCtx
     n::Int
     f!::Any          # f!(du, u, t)
@@ -478,7 +488,7 @@ function batch_reactor(input_file::AbstractString, lib_dir::AbstractString, user
     Mb = sum(x .* molwt)
     rho = inp.p * Mb / (R_GAS * inp.T)
     u0 = (x .* molwt ./ Mb) .* rho                                          # get_solution_vector (:224-232)
-    state = UserDefinedState(inp.T, inp.p, copy(x), molwt, names, zeros(ng))
+    state = _udf_state(inp.T, inp.p, copy(x), molwt, names, zeros(ng))
     chem = Chemistry(false, false, true, user_defined)
     residual! = (du, u, p, t) -> (user_defined(state); du[1:ng] .= state.source[1:ng] .* molwt; nothing)
     if sens
