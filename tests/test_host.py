@@ -363,3 +363,22 @@ def test_host_cvode_status_codes(pkg):
     with pytest.raises(ValueError):
         _lib.integrate_host(boom, [1.0], 1.0)
     assert _lib.integrate_host(f, [0.0, 0.0], -1.0)[0] == -10
+
+
+def test_host_cvode_robertson_against_scipy(pkg):
+    """br_integrate_host on a classic stiff problem that has nothing to do with the oracle (Robertson,
+    k1 = 0.04, k2 = 3e7, k3 = 1e4, t = 0..40): against SciPy's Radau at rtol 1e-10, the end state agrees
+    to the CVODE tolerance level (rtol 1e-6 / atol 1e-10), mass is conserved, and the DQ Jacobian path
+    is used (nje > 0, nfe_dq = n nje)."""
+    from scipy.integrate import solve_ivp
+    from batchreactor_amd import _lib
+
+    def f(t, y):
+        return np.array([-0.04 * y[0] + 1e4 * y[1] * y[2],
+                         0.04 * y[0] - 1e4 * y[1] * y[2] - 3e7 * y[1] ** 2,
+                         3e7 * y[1] ** 2])
+    status, u, st = _lib.integrate_host(f, [1.0, 0.0, 0.0], 40.0)
+    assert status == 0 and int(st[2]) > 0 and int(st[19]) == 3 * int(st[2])
+    ref = solve_ivp(f, (0.0, 40.0), [1.0, 0.0, 0.0], method="Radau", rtol=1e-10, atol=1e-14).y[:, -1]
+    assert np.all(np.abs(u - ref) <= 1e-4 * np.abs(ref) + 1e-9), (u, ref)
+    assert abs(u.sum() - 1.0) <= 1e-9
