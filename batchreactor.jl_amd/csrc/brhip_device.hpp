@@ -1138,8 +1138,17 @@ __device__ __forceinline__ void lu_rl_steps(double (&a)[W], int k0, int k1, int 
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
         const bool cand = pstep < 0;
-        const int p = pivot_lane(a[0], cand ? 0x7fffffffu : 0u, prow);
-        const double piv = bcast(a[0], p);
+        // rows sit in the previous factorization's pivot order, so step k's pivot is usually on lane k:
+        // when lane k is a candidate and no other candidate holds |a_ik| >= |a_kk|, lane k is the first
+        // max |a| of denseGETRF and the DPP max passes are skipped (ties or a larger entry: the full
+        // search). Round 6: bit-identical (scripts/bitcmp.py, GRI 4000 / surface 8000 reactors), GRI
+        // +0.6 %, surface-only +0.0 %; the same fast path in the CPL = 2 LU measured -0.2 % on C5
+        // (profiles/r06_lu_fastpiv_ab.json) and is not used there
+        const double akk = bcast(a[0], k);
+        const bool kcand = (__ballot(cand) >> k) & 1ull;
+        const bool fast = kcand && __ballot(cand && lane != k && !(fabs(a[0]) < fabs(akk))) == 0;
+        const int p = fast ? k : pivot_lane(a[0], cand ? 0x7fffffffu : 0u, prow);
+        const double piv = fast ? akk : bcast(a[0], p);
         if (piv == 0.0 && !fail) fail = k + 1;
         const double rinv = 1.0 / piv;
         const bool isp = (lane == p);

@@ -64,3 +64,34 @@ def test_pmc_traffic_summary(tmp_path):
                     str(tmp_path / "w.csv"), "8", str(out)], check=True, capture_output=True)
     d = json.loads(out.read_text())
     assert abs(d["bytes_per_reactor"] - (2 * 10.0 * 1024 + 4.0 * 1024) / 8) < 1e-9
+
+
+def test_parity_bounds_follow_the_committed_analysis():
+    """tests/parity_bands.py's bounds are the ones profiles/r06_parity_outliers.json derived (2x the
+    oracle's own spread on the bench samples, rounded up to 3 digits; analytic pre-ignition floors of
+    1e-6 bands and the surface bar of 1.0 as documented there), for every bench config and Jacobian,
+    and the GPU was inside them on every scored reactor of that analysis."""
+    import json
+    import math
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    import parity_bands as PB
+    d = json.load(open(os.path.join(root, "profiles", "r06_parity_outliers.json")))
+    for config, (ka, kd) in bench.PARITY_SAMPLE.items():
+        for jac, dq, k in (("analytic", False, ka), ("dq", True, kd)):
+            r = d["configs"][config][jac]
+            assert r["sample"] == k and r["gpu_frac_within_bound"] == 1.0
+            for w, (b, derived) in enumerate(zip(PB.BOUNDS[(config, dq)][:3], r["bound"])):
+                if config == "surf" and w > 0:
+                    continue                      # no ignition: only the pre-ignition window exists
+                if config == "surf" and not dq:
+                    assert b == 1.0 and max(r["gpu_vs_oracle"]["max"]) <= b
+                    continue
+                if w == 0 and not dq and config in ("gri", "h2o2"):
+                    assert b == 1e-6 and derived < b
+                    continue
+                assert derived <= b <= derived * (1 + 1e-2) + 1e-12, (config, jac, w, b, derived)
+                assert math.isfinite(b)
