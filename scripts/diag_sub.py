@@ -13,8 +13,7 @@ os.environ.setdefault("BRHIP_LIB", os.path.join(ROOT, "batchreactor.jl_amd", "li
 import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
-from batchreactor_amd import ensemble  # noqa: E402
-from bench import CONFIGS, make_mech  # noqa: E402
+from bench import CONFIGS, ensemble_inputs, make_mech  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "gri"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
@@ -27,7 +26,7 @@ mech = make_mech(pkg, cfg)
 eng = pkg.Engine(mech)
 lib = ctypes.CDLL(os.environ["BRHIP_LIB"])
 out = (ctypes.c_double * 16)()
-T, Asv, U0 = ensemble.make_inputs(mech, cfg, 0, N)
+T, Asv, U0 = ensemble_inputs(pkg, mech, cfg, N)
 lib.br_diag_sub(out)
 U, st = eng.integrate(T, Asv, U0, CONFIGS[cfg]["tf"])
 lib.br_diag_sub(out)

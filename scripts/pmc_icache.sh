@@ -14,7 +14,7 @@ c, n = sys.argv[1], int(sys.argv[2])
 tot = {}
 for f in glob.glob(f"gpurun_out/pmc_ic[12]_{c}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_integrate" in r["Kernel_Name"] or "k_lane" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in ("k_integrate", "k_lane", "k_group")):
             tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
 out = {"config": c, "reactors": n, "per_reactor": {k: v / n for k, v in tot.items()}}
 if tot.get("SQC_ICACHE_REQ"):
