@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import LIB
+from conftest import LIB, ROOT
 
 pytestmark = pytest.mark.gpu
 TH = os.path.join(LIB, "therm.dat")
@@ -374,6 +374,42 @@ def test_batched_lu_solve_mfma(pkg, gpu, n):
         A = np.eye(n) - g[i] * J[i]
         res = A @ x[i] - b[i]
         assert np.max(np.abs(res)) <= 1e-12 * (np.abs(A).sum(1).max() * np.abs(x[i]).max() + np.abs(b[i]).max())
+
+
+def test_coop_lu_solve_bit_identical(pkg, gpu):
+    """The cooperative-engine experiment (scripts/micro/coop_lusolve.hip, not
+    part of libbrhip.so; profiles/r06_coop_ab.json): the LU factors held in the registers of a 4-wave
+    workgroup, with a barrier per step or per 16-column panel, give bit-for-bit the integrator's
+    lu_factor<56> / lu_solve<56> results (pivoting included: scaled random matrices, the first LU in
+    natural row order, later ones in the previous pivot order), within the backward-error bound."""
+    import ctypes as C
+    path = os.path.join(ROOT, "scripts", "micro", "libcoop.so")
+    assert os.path.exists(path), "experiment library not built (make -C scripts/micro libcoop.so)"
+    lib = C.CDLL(path)
+    dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int)
+    lib.coop_run.argtypes = [C.c_int, C.c_int, C.c_int, dp, C.c_int, dp, dp, C.c_int, C.c_int, dp, dp, ip, dp, ip]
+    rng = np.random.default_rng(11)
+    n, N, nj, reps, nsolve = 53, 256, 64, 2, 3
+    J = np.ascontiguousarray(rng.standard_normal((nj, n, n)) * np.exp(rng.uniform(-8, 8, (nj, n, 1))))
+    g = np.ascontiguousarray(np.exp(rng.uniform(-12, -2, N)))
+    b = np.ascontiguousarray(rng.standard_normal((N, n)))
+    P = lambda a: a.ctypes.data_as(dp)  # noqa: E731
+    outs = {}
+    for mode in (0, 1, 3):
+        x, chk, f = np.zeros((N, n)), np.zeros((N, n)), np.zeros(N, np.int32)
+        ms, vg = C.c_double(0.0), C.c_int(0)
+        assert lib.coop_run(mode, N, n, P(J), nj, P(g), P(b), reps, nsolve, P(x), P(chk), f.ctypes.data_as(ip),
+                            C.byref(ms), C.byref(vg)) == 0
+        assert np.all(f == 0)
+        outs[mode] = (x, chk)
+    for mode in (1, 3):
+        assert np.array_equal(outs[mode][0].view(np.int64), outs[0][0].view(np.int64)), mode
+        assert np.array_equal(outs[mode][1].view(np.int64), outs[0][1].view(np.int64)), mode
+    x = outs[0][0]
+    for i in range(0, N, 17):
+        A = np.eye(n) - g[i] * J[i % nj]
+        res = A @ x[i] - b[i] * nsolve
+        assert np.max(np.abs(res)) <= 1e-12 * (np.abs(A).sum(1).max() * np.abs(x[i]).max() + nsolve * np.abs(b[i]).max())
 
 
 def test_gas_surf_golden_early_steps(pkg, gpu):
