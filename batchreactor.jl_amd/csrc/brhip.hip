@@ -36,6 +36,16 @@
 #define BR_X_AFTER_SOLVE()
 #define BR_X_AFTER_ITER()
 #endif
+#ifndef BR_XC_AFTER_CVSET   // ... and inside the controller (cvSet, the step-size ratio root)
+#define BR_XC_AFTER_CVSET()
+#define BR_XC_AFTER_ETAQ()
+#endif
+#ifndef BR_XG_AFTER_RHS   // the same for k_group (brhip_group.hpp)
+#define BR_XG_AFTER_RHS()
+#define BR_XG_AFTER_JAC()
+#define BR_XG_AFTER_LU()
+#define BR_XG_AFTER_SOLVE()
+#endif
 
 using namespace brhip;
 
@@ -371,8 +381,10 @@ __device__ __forceinline__ void dense_output(LCtl* C, VA<CPL, GW, VS>& V, const 
 }
 
 // 1.0 / j for the small integers of the BDF coefficient formulas (exactly the rounded quotient)
+// (j is in 1 .. QMAX + 1 at every call site; no run-time division for the impossible rest: with
+// per-lane j it was evaluated on every call, ~11 VALU each)
 __device__ __forceinline__ double inv_int(int j) {
-    return j == 1 ? 1.0 : j == 2 ? 0.5 : j == 3 ? 1.0 / 3.0 : j == 4 ? 0.25 : j == 5 ? 0.2 : j == 6 ? 1.0 / 6.0 : 1.0 / j;
+    return j == 1 ? 1.0 : j == 2 ? 0.5 : j == 3 ? 1.0 / 3.0 : j == 4 ? 0.25 : j == 5 ? 0.2 : 1.0 / 6.0;
 }
 
 // the controller scalars one attempt (predict + cvSet) reads, loaded in one batch before the
@@ -474,6 +486,116 @@ __device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4
     C->gamma = gamma;
     if (nst == 0) C->gammap = gamma;
     gamrat_out = (nst > 0) ? gamma / in.gammap : 1.0;
+    C->gamrat = gamrat_out;
+}
+
+// cvSet for the 16-lane groups of k_group<16, NM> (GW = 16): cv_set's operations, with the independent
+// divisions spread over the lanes of the group -- lane t of the DPP row computes one quotient and a
+// row broadcast (row_newbcast) hands it to the row, 3 division sequences instead of 14 -- and the
+// order masks of the l recurrences folded into zero coefficients (exact: every l_i is >= 0 and
+// finite, so l_i + l_{i-1} * 0 = l_i). C2: cv_set was 19 % of the kernel's VALU instructions
+// (profiles/r06_quad_valu_split.json). On the same inputs it returns cv_set's bits
+// (scripts/micro/cvset_check.hip, 8192 random states); inside the integrator the compiler fuses
+// multiplies and adds of the surrounding code differently, so C2 trajectories move by rounding
+// (< 0.5 band against the previous build, parity windows unchanged).
+template <int K>
+__device__ __forceinline__ double row_lane(double v) { return dppd<0x150 + K>(v); }
+__device__ __forceinline__ double sel6(int t, double v0, double v1, double v2, double v3, double v4, double v5) {
+    // lane t's operand (opaque copies: a select chain, not a private array in scratch memory)
+    double v = v0;
+    const double c[5] = {v1, v2, v3, v4, v5};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        double x = c[i];
+        asm volatile("" : "+v"(x));
+        v = (t == i + 1) ? x : v;
+    }
+    return v;
+}
+__device__ __forceinline__ void cv_set_g16(LCtl* C, const AttemptIn& in, double& tq4_out, double& gamrat_out) {
+    const int t = (int)(threadIdx.x & 15);
+    const int q = in.q, qwait = in.qwait, nst = in.nst;
+    const double h = in.h;
+    // h / hsum_m, hsum_m = h + tau[1] + ... + tau[m-1] in CVODE's order, m = 2 .. QMAX + 1: lane m - 2
+    double hsum[QMAX + 2];
+    {
+        double hs = h;
+#pragma unroll
+        for (int m = 2; m <= QMAX + 1; ++m) {
+            hs += in.tau[m - 1];
+            hsum[m] = hs;
+        }
+    }
+    const double xq = h / sel6(t, hsum[2], hsum[3], hsum[4], hsum[5], hsum[6], hsum[6]);
+    double xinv[QMAX + 2];
+    xinv[0] = xinv[1] = 0.0;
+    xinv[2] = row_lane<0>(xq); xinv[3] = row_lane<1>(xq); xinv[4] = row_lane<2>(xq);
+    xinv[5] = row_lane<3>(xq); xinv[6] = row_lane<4>(xq);
+    auto pick = [&](const double* arr, int lo, int hi, int m) {
+        double v = arr[lo];
+#pragma unroll
+        for (int i = lo + 1; i <= QMAX + 1; ++i) {
+            if (i <= hi) {
+                double x = arr[i];
+                asm volatile("" : "+v"(x));
+                v = (m == i) ? x : v;
+            }
+        }
+        return v;
+    };
+    double lv[QMAX + 1] = {1.0, 1.0, 0.0, 0.0, 0.0, 0.0};
+    double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0;
+    if (q > 1) {
+#pragma unroll
+        for (int j = 2; j < QMAX; ++j) {
+            const bool on = j < q;
+            const double c = on ? xinv[j] : 0.0;
+            alpha0 -= on ? inv_int(j) : 0.0;
+#pragma unroll
+            for (int i = QMAX; i >= 1; --i) if (i <= j) lv[i] += lv[i - 1] * c;
+        }
+        alpha0 -= inv_int(q);
+        xistar_inv = -lv[1] - alpha0;
+        xi_inv = pick(xinv, 2, QMAX + 1, q);
+        alpha0_hat = -lv[1] - xi_inv;
+        // no order mask: l_i = 0 for i >= q here, and the descending sweep reads each l_{i-1} before
+        // updating it, so every l_i with i > q stays 0 (0 + 0 * xistar_inv)
+#pragma unroll
+        for (int i = QMAX; i >= 1; --i) lv[i] += lv[i - 1] * xistar_inv;
+    }
+#pragma unroll
+    for (int i = 0; i <= QMAX; ++i) C->l[i] = lv[i];
+    const double A1 = 1.0 - alpha0_hat + alpha0;
+    const double A2 = 1.0 + q * A1;
+    const double lq = pick(lv, 1, QMAX, q);
+    // round 1, lane t: 0 tq2, 1 tq5, 2 1/l_1, 3 Cc, 4 Cpinv, 5 Cppinv (3..5 used when qwait == 1)
+    const double A3 = alpha0 + inv_int(q);
+    const double A4 = alpha0_hat + xi_inv;
+    const double xi1 = pick(xinv, 2, QMAX + 1, q + 1);   // h / (h + tau[1] + ... + tau[q])
+    const double A5 = alpha0 - inv_int(q + 1);
+    const double A6 = alpha0_hat - xi1;
+    const double num = sel6(t, A1, A2 * xistar_inv, 1.0, xistar_inv, 1.0 - A4 + A3, 1.0 - A6 + A5);
+    const double den = sel6(t, alpha0 * A2, lq * xi_inv, lv[1], lq, A3, A2);
+    const double r1 = num / den;
+    const double tq2 = fabs(row_lane<0>(r1));
+    const double rl1 = row_lane<2>(r1);
+    const double Cc = row_lane<3>(r1), Cpinv = row_lane<4>(r1), Cppinv = row_lane<5>(r1);
+    C->tq[2] = tq2;
+    C->tq[5] = fabs(row_lane<1>(r1));
+    C->rl1 = rl1;
+    const double gamma = h * rl1;
+    C->gamma = gamma;
+    if (nst == 0) C->gammap = gamma;
+    // round 2, lane t: 0 tq4, 1 tq3's quotient, 2 gamrat
+    const double r2 = sel6(t, CORTES, Cppinv, gamma, 1.0, 1.0, 1.0) /
+                      sel6(t, tq2, xi1 * (q + 2) * A5, in.gammap, 1.0, 1.0, 1.0);
+    tq4_out = row_lane<0>(r2);
+    C->tq[4] = tq4_out;
+    if (qwait == 1) {
+        C->tq[1] = (q > 1) ? fabs(Cc * Cpinv) : 1.0;
+        C->tq[3] = fabs(row_lane<1>(r2));
+    }
+    gamrat_out = (nst > 0) ? row_lane<2>(r2) : 1.0;
     C->gamrat = gamrat_out;
 }
 
@@ -595,7 +717,9 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL, GW, VS>& V, int l
     const AttemptIn in = load_attempt<GW>(C);
     cv_predict<CPL, GW>(C, V, lane, in);
     double tq4, gamrat;
-    cv_set<GW>(C, in, tq4, gamrat);
+    if constexpr (GW == 16) cv_set_g16(C, in, tq4, gamrat);
+    else cv_set<GW>(C, in, tq4, gamrat);
+    BR_XC_AFTER_CVSET();
     const int nst = in.nst;
     C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
     C->callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
@@ -934,8 +1058,62 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL, GW, VS>& V, int lan
     int qprime = q;
     if (etamax == 1.0) {
         qwait = qwait > 2 ? qwait : 2;
+    } else if constexpr (GW == 16) {
+        // the three step-size ratios (etaq, and at an order decision etaqm1 / etaqp1) in ONE root and
+        // division sequence: lane 0 of the group takes etaq's argument, lane 1 etaqm1's, lane 2
+        // etaqp1's (root_int and the division per lane; a DPP row broadcast returns each); C2: etaq's
+        // root + division alone was 4.6 % of the kernel's VALU (profiles/r06_quad_valu_split.json)
+        const int t = lane & 15;
+        double xm = 1.0, xp = 1.0;     // benign arguments for lanes whose ratio is not needed
+        bool hm = false, hp = false;
+        if (qwait == 0) {
+            if (q > 1) {
+                double zq[CPL];
+#pragma unroll
+                FOR_S zq[s] = vget<CPL>(V, q, s);
+                const double ddn = wrms_l<CPL, GW>(zq, ewt, lane, n) * tq1;
+                xm = BIAS1 * ddn;
+                hm = true;
+            }
+            if (q != QMAX && saved_tq5 != 0.0) {
+                const double cquot = (tq5 / saved_tq5) * pow_int(h / tau2, L);
+                double tempv[CPL];
+#pragma unroll
+                FOR_S tempv[s] = acor[s] - cquot * V.at(QMAX, s);
+                const double dup = wrms_l<CPL, GW>(tempv, ewt, lane, n) * tq3;
+                xp = BIAS3 * dup;
+                hp = true;
+            }
+        }
+        const double xa = t == 1 ? xm : (t == 2 ? xp : BIAS2 * dsm);
+        const int La = t == 1 ? (hm ? q : L) : (t == 2 ? (hp ? L + 1 : L) : L);
+        const double er = 1.0 / (root_int(xa, La) + ADDON);
+        const double etaq = row_lane<0>(er);
+        BR_XC_AFTER_ETAQ();
+        if (qwait != 0) { eta = etaq; }
+        else {
+            qwait = 2;
+            const double etaqm1 = hm ? row_lane<1>(er) : 0.0;
+            const double etaqp1 = hp ? row_lane<2>(er) : 0.0;
+            const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
+            if (etam < THRESH) { eta = 1.0; }
+            else if (etam == etaq) { eta = etaq; }
+            else if (etam == etaqm1) { eta = etaqm1; qprime = q - 1; }
+            else {
+                eta = etaqp1; qprime = q + 1;
+#pragma unroll
+                FOR_S V.at(QMAX, s) = acor[s];
+            }
+        }
+        if (eta < THRESH) { eta = 1.0; hprime = h; }                // cvSetEta
+        else {
+            eta = fmin(eta, etamax);
+            if (a.hmax_inv > 0) eta /= fmax(1.0, fabs(h) * a.hmax_inv * eta);   // (/ 1.0 otherwise)
+            hprime = h * eta;
+        }
     } else {
         const double etaq = 1.0 / (root_int(BIAS2 * dsm, L) + ADDON);
+        BR_XC_AFTER_ETAQ();
         if (qwait != 0) { eta = etaq; }
         else {
             qwait = 2;
@@ -968,7 +1146,7 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL, GW, VS>& V, int lan
         if (eta < THRESH) { eta = 1.0; hprime = h; }                // cvSetEta
         else {
             eta = fmin(eta, etamax);
-            eta /= fmax(1.0, fabs(h) * a.hmax_inv * eta);
+            if (a.hmax_inv > 0) eta /= fmax(1.0, fabs(h) * a.hmax_inv * eta);   // (/ 1.0 otherwise)
             hprime = h * eta;
         }
     }

@@ -674,6 +674,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
             }
             QCLK(c_r);
             const double fv = g_rhs<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, yv, gl, p_last);
+            BR_XG_AFTER_RHS();
             QACC(q_rhs_c, c_r);
             double f[1] = {fv}, b[1];
             int act_code;
@@ -715,6 +716,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
                     g_jac_cols<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, gl, jst);   // column passes
 #pragma unroll 1
                     for (int j = n; j < NM; ++j) jst(j, 0.0);                 // padding columns
+                    BR_XG_AFTER_JAC();
                     QACC(q_jac_c, c_j);
                 }
                 QCLK(c_l);
@@ -722,6 +724,7 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
 #pragma unroll
                 for (int j = 0; j < NM; ++j) jr[j] = jld(j);
                 lu_fail = g_lu<GL, NM>(jr, C->gamma, n, gl, a, orig, dinv);
+                BR_XG_AFTER_LU();
                 QACC(q_lu_c, c_l);
 #if BR_GPRIO
                 __builtin_amdgcn_s_setprio(0);
@@ -730,7 +733,10 @@ __global__ __launch_bounds__(64 * BR_QWPB) __attribute__((amdgpu_waves_per_eu(GL
             if (act_code == A_SOLVE || act_code == A_SETUP) {
                 QCLK(c_s);
                 double delta[1] = {0.0};
-                if (!lu_fail) delta[0] = g_solve<GL, NM>(a, orig, dinv, n, gl, b[0]);
+                if (!lu_fail) {
+                    delta[0] = g_solve<GL, NM>(a, orig, dinv, n, gl, b[0]);
+                    BR_XG_AFTER_SOLVE();
+                }
                 QACC(q_sol_c, c_s);
                 QCLK(c_p);
                 BR_SUB_T(ps_all);

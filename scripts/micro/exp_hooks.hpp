@@ -7,7 +7,88 @@
 //   BR_EXP_VALU=K    : K independent dummy fp64 FMAs per Newton iteration (VALU-issue sensitivity)
 //   BR_EXP_MEM=K     : K columns (512 B each) of the saved J re-read per Newton iteration (memory-
 //                      side sensitivity)
+//   BR_EXP_GDUP=1/2/3/4 : k_group (group engines): the RHS / the solve / the Jacobian / the LU run
+//                      twice (scripts/gdup_valu.sh)
 #pragma once
+
+//   BR_EXP_CDUP=1/2    : in the 16-lane groups' controller, cvSet / the etaq ratio (root_int + the
+//                      division) evaluated twice on opaque copies of their inputs
+#if defined(BR_EXP_CDUP) && BR_EXP_CDUP == 1
+#define BR_XC_AFTER_CVSET()                                                                  \
+    do {                                                                                     \
+        if constexpr (GW == 16) {                                                            \
+            AttemptIn in2 = in;                                                              \
+            asm volatile("" : "+v"(in2.q), "+v"(in2.qwait), "+v"(in2.nst), "+v"(in2.h));     \
+            asm volatile("" : "+v"(in2.gammap), "+v"(in2.tau[1]), "+v"(in2.tau[2]));          \
+            asm volatile("" : "+v"(in2.tau[3]), "+v"(in2.tau[4]), "+v"(in2.tau[5]), "+v"(in2.tau[6])); \
+            double t4b, grb;                                                                 \
+            cv_set<GW>(C, in2, t4b, grb);                                                    \
+            asm volatile("" ::"v"(t4b), "v"(grb));                                           \
+        }                                                                                    \
+    } while (0)
+#endif
+#if defined(BR_EXP_CDUP) && BR_EXP_CDUP == 2
+#define BR_XC_AFTER_ETAQ()                                                                   \
+    do {                                                                                     \
+        if constexpr (GW == 16) {                                                            \
+            double x2 = BIAS2 * dsm;                                                         \
+            int L2 = L;                                                                      \
+            asm volatile("" : "+v"(x2), "+v"(L2));                                           \
+            const double e2 = 1.0 / (root_int(x2, L2) + ADDON);                              \
+            asm volatile("" ::"v"(e2));                                                      \
+        }                                                                                    \
+    } while (0)
+#endif
+#if defined(BR_EXP_CDUP)
+#ifndef BR_XC_AFTER_CVSET
+#define BR_XC_AFTER_CVSET()
+#endif
+#ifndef BR_XC_AFTER_ETAQ
+#define BR_XC_AFTER_ETAQ()
+#endif
+#endif
+
+#if defined(BR_EXP_GDUP) && BR_EXP_GDUP == 1
+#define BR_XG_AFTER_RHS()                                                                    \
+    do {                                                                                     \
+        asm volatile("" ::: "memory");                                                       \
+        double f2 = g_rhs<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, yv, gl, p_last);         \
+        asm volatile("" ::"v"(f2));                                                          \
+    } while (0)
+#else
+#define BR_XG_AFTER_RHS()
+#endif
+#if defined(BR_EXP_GDUP) && BR_EXP_GDUP == 2
+#define BR_XG_AFTER_SOLVE()                                                                  \
+    do {                                                                                     \
+        asm volatile("" ::"v"(delta[0]) : "memory");   /* the first solve stays live */      \
+        double bb = b[0];                                                                    \
+        asm volatile("" : "+v"(bb));   /* opaque: the two solves cannot be merged */           \
+        double d2 = g_solve<GL, NM>(a, orig, dinv, n, gl, bb);                               \
+        asm volatile("" : "+v"(d2));                                                         \
+        delta[0] = d2;                                                                       \
+    } while (0)
+#else
+#define BR_XG_AFTER_SOLVE()
+#endif
+#if defined(BR_EXP_GDUP) && BR_EXP_GDUP == 3
+#define BR_XG_AFTER_JAC()                                                                    \
+    do {                                                                                     \
+        asm volatile("" ::: "memory");                                                       \
+        g_jac_cols<GL>(tb, sp, kd, fod, skd, T, Asv, Asv_th, gl, jst);                       \
+    } while (0)
+#else
+#define BR_XG_AFTER_JAC()
+#endif
+#if defined(BR_EXP_GDUP) && BR_EXP_GDUP == 4
+#define BR_XG_AFTER_LU()                                                                     \
+    do {                                                                                     \
+        asm volatile("" ::: "memory");                                                       \
+        lu_fail = g_lu<GL, NM>(jr, C->gamma, n, gl, a, orig, dinv);                          \
+    } while (0)
+#else
+#define BR_XG_AFTER_LU()
+#endif
 
 #if defined(BR_EXP_DUP) && BR_EXP_DUP == 1
 #define BR_X_AFTER_RHS()                                                \
