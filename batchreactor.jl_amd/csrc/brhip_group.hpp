@@ -487,9 +487,15 @@ __device__ __forceinline__ int g_lu(const double (&jr)[NM], double gamma, int n,
             const double l = below ? a[k] * rinv : 0.0;                  // denseGETRF: a_ik *= 1 / a_kk
             if (below) a[k] = l;
             if (gl == k) dinv = rinv;
+            // 16-lane groups: the pivot-row value enters the FMA as its DPP operand (v_fmac_f64_dpp
+            // row_newbcast:k, the rows of all groups at once): one VALU op per element instead of two
+            // DPP moves and an FMA; fma(u_kj, -l, a_ij) is fma(-u_kj, l, a_ij) exactly
 #pragma unroll
             for (int j = k + 1; j < NM; ++j)
-                if (j < n) a[j] = fma(-group_bcast<GL, k>(a[j]), l, a[j]);
+                if (j < n) {
+                    if constexpr (GL == 16) dpp_fnma_self<k, 0xF>(a[j], l);
+                    else a[j] = fma(-group_bcast<GL, k>(a[j]), l, a[j]);
+                }
         }
     });
     return fail;
@@ -505,8 +511,12 @@ __device__ __forceinline__ double g_solve(const double (&a)[NM], int orig, doubl
     sfor<0, NM>([&](auto kc) {                                          // L y = P b
         constexpr int k = decltype(kc)::value;
         if (k + 1 < n) {
-            const double yk = group_bcast<GL, k>(y);
-            y = fma(-((gl > k) ? a[k] : 0.0), yk, y);
+            if constexpr (GL == 16) {
+                dpp_fnma_self<k, 0xF>(y, (gl > k) ? a[k] : 0.0);   // y += -l_sk y_k, y_k as the DPP operand
+            } else {
+                const double yk = group_bcast<GL, k>(y);
+                y = fma(-((gl > k) ? a[k] : 0.0), yk, y);
+            }
         }
     });
     double x = 0.0;
@@ -514,8 +524,12 @@ __device__ __forceinline__ double g_solve(const double (&a)[NM], int orig, doubl
         constexpr int k = NM - 1 - decltype(kc)::value;
         if (k < n) {
             if (gl == k) x = y * dinv;
-            const double xk = group_bcast<GL, k>(x);
-            y = fma(-((gl < k) ? a[k] : 0.0), xk, y);
+            if constexpr (GL == 16) {
+                dpp_fnma<k, 0xF, true>(y, x, (gl < k) ? a[k] : 0.0);   // y += -u_sk x_k
+            } else {
+                const double xk = group_bcast<GL, k>(x);
+                y = fma(-((gl < k) ? a[k] : 0.0), xk, y);
+            }
         }
     });
     return gl < n ? x : 0.0;
