@@ -489,15 +489,17 @@ __device__ __forceinline__ void cv_set(LCtl* C, const AttemptIn& in, double& tq4
     C->gamrat = gamrat_out;
 }
 
-// cvSet for the 16-lane groups of k_group<16, NM> (GW = 16): cv_set's operations, with the independent
-// divisions spread over the lanes of the group -- lane t of the DPP row computes one quotient and a
-// row broadcast (row_newbcast) hands it to the row, 3 division sequences instead of 14 -- and the
-// order masks of the l recurrences folded into zero coefficients (exact: every l_i is >= 0 and
-// finite, so l_i + l_{i-1} * 0 = l_i). C2: cv_set was 19 % of the kernel's VALU instructions
+// cvSet in every engine (cv_set_lp): cv_set's operations, with the independent divisions spread over
+// the lanes of each 16-lane DPP row -- lane t computes one quotient and a row broadcast
+// (row_newbcast) hands it to the row (a 16-lane group is one row; in 32- and 64-lane groups every
+// row computes the same quotients), 3 division sequences instead of 14 -- and the order masks of the
+// l recurrences folded into zero coefficients (exact: every l_i is >= 0 and finite, so
+// l_i + l_{i-1} * 0 = l_i). cv_set was 19 % of C2's VALU instructions and 7.1 % of GRI's
 // (profiles/r06_quad_valu_split.json). On the same inputs it returns cv_set's bits
-// (scripts/micro/cvset_check.hip, 8192 random states); inside the integrator the compiler fuses
-// multiplies and adds of the surrounding code differently, so C2 trajectories move by rounding
-// (< 0.5 band against the previous build, parity windows unchanged).
+// (scripts/micro/cvset_check.hip, 8192 random states), and the wavefront engine's trajectories are
+// bit-identical to the cv_set build (GRI, surface-only, gas + surface); inside k_group the compiler
+// fuses multiplies and adds of the surrounding code differently, so C2 trajectories move by
+// rounding (< 0.5 band against the cv_set build, parity windows unchanged).
 template <int K>
 __device__ __forceinline__ double row_lane(double v) { return dppd<0x150 + K>(v); }
 __device__ __forceinline__ double sel6(int t, double v0, double v1, double v2, double v3, double v4, double v5) {
@@ -512,7 +514,7 @@ __device__ __forceinline__ double sel6(int t, double v0, double v1, double v2, d
     }
     return v;
 }
-__device__ __forceinline__ void cv_set_g16(LCtl* C, const AttemptIn& in, double& tq4_out, double& gamrat_out) {
+__device__ __forceinline__ void cv_set_lp(LCtl* C, const AttemptIn& in, double& tq4_out, double& gamrat_out) {
     const int t = (int)(threadIdx.x & 15);
     const int q = in.q, qwait = in.qwait, nst = in.nst;
     const double h = in.h;
@@ -717,8 +719,7 @@ __device__ __forceinline__ void begin_attempt(LCtl* C, VA<CPL, GW, VS>& V, int l
     const AttemptIn in = load_attempt<GW>(C);
     cv_predict<CPL, GW>(C, V, lane, in);
     double tq4, gamrat;
-    if constexpr (GW == 16) cv_set_g16(C, in, tq4, gamrat);
-    else cv_set<GW>(C, in, tq4, gamrat);
+    cv_set_lp(C, in, tq4, gamrat);   // (cv_set: the plain form it is checked against)
     BR_XC_AFTER_CVSET();
     const int nst = in.nst;
     C->convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? NO_FAILURES : FAIL_OTHER;
@@ -1058,10 +1059,10 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL, GW, VS>& V, int lan
     int qprime = q;
     if (etamax == 1.0) {
         qwait = qwait > 2 ? qwait : 2;
-    } else if constexpr (GW == 16) {
+    } else {
         // the three step-size ratios (etaq, and at an order decision etaqm1 / etaqp1) in ONE root and
-        // division sequence: lane 0 of the group takes etaq's argument, lane 1 etaqm1's, lane 2
-        // etaqp1's (root_int and the division per lane; a DPP row broadcast returns each); C2: etaq's
+        // division sequence: lane 0 of each DPP row takes etaq's argument, lane 1 etaqm1's, lane 2
+        // etaqp1's (root_int and the division per lane; a row broadcast returns each); C2: etaq's
         // root + division alone was 4.6 % of the kernel's VALU (profiles/r06_quad_valu_split.json)
         const int t = lane & 15;
         double xm = 1.0, xp = 1.0;     // benign arguments for lanes whose ratio is not needed
@@ -1095,44 +1096,6 @@ __device__ BR_CTL_INLINE int ctl_post_solve(LCtl* C, VA<CPL, GW, VS>& V, int lan
             qwait = 2;
             const double etaqm1 = hm ? row_lane<1>(er) : 0.0;
             const double etaqp1 = hp ? row_lane<2>(er) : 0.0;
-            const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
-            if (etam < THRESH) { eta = 1.0; }
-            else if (etam == etaq) { eta = etaq; }
-            else if (etam == etaqm1) { eta = etaqm1; qprime = q - 1; }
-            else {
-                eta = etaqp1; qprime = q + 1;
-#pragma unroll
-                FOR_S V.at(QMAX, s) = acor[s];
-            }
-        }
-        if (eta < THRESH) { eta = 1.0; hprime = h; }                // cvSetEta
-        else {
-            eta = fmin(eta, etamax);
-            if (a.hmax_inv > 0) eta /= fmax(1.0, fabs(h) * a.hmax_inv * eta);   // (/ 1.0 otherwise)
-            hprime = h * eta;
-        }
-    } else {
-        const double etaq = 1.0 / (root_int(BIAS2 * dsm, L) + ADDON);
-        BR_XC_AFTER_ETAQ();
-        if (qwait != 0) { eta = etaq; }
-        else {
-            qwait = 2;
-            double etaqm1 = 0.0, etaqp1 = 0.0;
-            if (q > 1) {
-                double zq[CPL];
-#pragma unroll
-                FOR_S zq[s] = vget<CPL>(V, q, s);
-                const double ddn = wrms_l<CPL, GW>(zq, ewt, lane, n) * tq1;
-                etaqm1 = 1.0 / (root_int(BIAS1 * ddn, q) + ADDON);
-            }
-            if (q != QMAX && saved_tq5 != 0.0) {
-                const double cquot = (tq5 / saved_tq5) * pow_int(h / tau2, L);
-                double tempv[CPL];
-#pragma unroll
-                FOR_S tempv[s] = acor[s] - cquot * V.at(QMAX, s);
-                const double dup = wrms_l<CPL, GW>(tempv, ewt, lane, n) * tq3;
-                etaqp1 = 1.0 / (root_int(BIAS3 * dup, L + 1) + ADDON);
-            }
             const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
             if (etam < THRESH) { eta = 1.0; }
             else if (etam == etaq) { eta = etaq; }

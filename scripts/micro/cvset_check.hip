@@ -1,4 +1,4 @@
-// cvset_check.hip -- device-side check that the 16-lane groups' lane-parallel cvSet (cv_set_g16) and
+// cvset_check.hip -- device-side check that the 16-lane groups' lane-parallel cvSet (cv_set_lp) and
 // step-size ratios give bit-for-bit the values of the generic forms (cv_set<16>, one root_int per
 // ratio) on random controller states. Includes the whole integrator translation unit; not part of
 // libbrhip.so.   python3 scripts/cvset_check.py
@@ -25,7 +25,7 @@ __global__ __launch_bounds__(64) void k_cvchk(int ncase, const double* __restric
     wave_sync();
     double t4a, gra, t4b, grb;
     cv_set<16>(C0, in, t4a, gra);
-    cv_set_g16(C1, in, t4b, grb);
+    cv_set_lp(C1, in, t4b, grb);
     wave_sync();
     // the step-size ratios: lane 0 etaq (L), lane 1 etaqm1 (q), lane 2 etaqp1 (L + 1), as ctl_post_solve
     const double dsm = din[10 * cc + 9], ddn = 0.7 * dsm + 1e-3, dup = 1.3 * dsm + 2e-3;

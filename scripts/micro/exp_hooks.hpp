@@ -27,6 +27,20 @@
         }                                                                                    \
     } while (0)
 #endif
+#if defined(BR_EXP_CDUP) && BR_EXP_CDUP == 3   // the wavefront engine's cvSet (GW = 64)
+#define BR_XC_AFTER_CVSET()                                                                  \
+    do {                                                                                     \
+        if constexpr (GW == 64) {                                                            \
+            AttemptIn in2 = in;                                                              \
+            asm volatile("" : "+s"(in2.q), "+s"(in2.qwait), "+s"(in2.nst));                  \
+            asm volatile("" : "+v"(in2.h), "+v"(in2.gammap), "+v"(in2.tau[1]), "+v"(in2.tau[2])); \
+            asm volatile("" : "+v"(in2.tau[3]), "+v"(in2.tau[4]), "+v"(in2.tau[5]), "+v"(in2.tau[6])); \
+            double t4b, grb;                                                                 \
+            cv_set<GW>(C, in2, t4b, grb);                                                    \
+            asm volatile("" ::"v"(t4b), "v"(grb));                                           \
+        }                                                                                    \
+    } while (0)
+#endif
 #if defined(BR_EXP_CDUP) && BR_EXP_CDUP == 2
 #define BR_XC_AFTER_ETAQ()                                                                   \
     do {                                                                                     \
