@@ -412,6 +412,36 @@ def test_coop_lu_solve_bit_identical(pkg, gpu):
         assert np.max(np.abs(res)) <= 1e-12 * (np.abs(A).sum(1).max() * np.abs(x[i]).max() + nsolve * np.abs(b[i]).max())
 
 
+def test_cvset_lane_parallel_matches_plain(gpu):
+    """The lane-parallel BDF coefficient update (cv_set_lp: independent divisions spread over the
+    lanes of a DPP row, row broadcasts, zero coefficients for unused orders) and the shared root of
+    the three step-size ratios return the plain forms' bits (cv_set, one root_int per ratio) on random
+    controller states of every order / qwait / nst case (scripts/micro/cvset_check.hip, the whole
+    integrator translation unit)."""
+    import ctypes as C
+    path = os.path.join(ROOT, "scripts", "micro", "libcvset_check.so")
+    assert os.path.exists(path), "check library not built (make -C scripts/micro libcvset_check.so)"
+    N = 4096
+    rng = np.random.default_rng(3)
+    iin = np.zeros((N, 4), np.int32)
+    iin[:, 0] = rng.integers(1, 6, N)
+    iin[:, 1] = rng.integers(0, 3, N)
+    iin[:, 2] = rng.choice([0, 7], N)
+    din = np.zeros((N, 10))
+    h = 10.0 ** rng.uniform(-9, -2, N)
+    din[:, 0] = h
+    din[:, 1] = h * rng.uniform(0.06, 1.5, N)
+    for i in range(1, 7):
+        din[:, 2 + i] = h * rng.uniform(0.3, 3.0, N)
+    din[:, 9] = 10.0 ** rng.uniform(-3, 1, N)
+    out = np.zeros((N, 16, 2, 16))
+    lib = C.CDLL(path)
+    assert lib.cvset_check(N, din.ctypes.data_as(C.c_void_p), iin.ctypes.data_as(C.c_void_p),
+                           out.ctypes.data_as(C.c_void_p)) == 0
+    a, b = out[:, :, 0, :], out[:, :, 1, :]
+    assert np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
 def test_gas_surf_golden_early_steps(pkg, gpu):
     """The reference's own gas+surface output (test/batch_gas_and_surf, GRI + ch4ni, T = 1173 K,
     Asv = 1, rtol 1e-6 / atol 1e-10; tests/golden/gas_and_surf_*golden.csv) against the engine's
