@@ -22,7 +22,7 @@
             asm volatile("" : "+v"(in2.gammap), "+v"(in2.tau[1]), "+v"(in2.tau[2]));          \
             asm volatile("" : "+v"(in2.tau[3]), "+v"(in2.tau[4]), "+v"(in2.tau[5]), "+v"(in2.tau[6])); \
             double t4b, grb;                                                                 \
-            cv_set<GW>(C, in2, t4b, grb);                                                    \
+            cv_set_lp(C, in2, t4b, grb);                                                     \
             asm volatile("" ::"v"(t4b), "v"(grb));                                           \
         }                                                                                    \
     } while (0)
@@ -36,7 +36,7 @@
             asm volatile("" : "+v"(in2.h), "+v"(in2.gammap), "+v"(in2.tau[1]), "+v"(in2.tau[2])); \
             asm volatile("" : "+v"(in2.tau[3]), "+v"(in2.tau[4]), "+v"(in2.tau[5]), "+v"(in2.tau[6])); \
             double t4b, grb;                                                                 \
-            cv_set<GW>(C, in2, t4b, grb);                                                    \
+            cv_set_lp(C, in2, t4b, grb);                                                     \
             asm volatile("" ::"v"(t4b), "v"(grb));                                           \
         }                                                                                    \
     } while (0)
